@@ -1,0 +1,370 @@
+// libgz_nn.so -- C-ABI (include/gzero_nn.h) around the fused gfx950 forward kernel.
+//
+// Host side: parses the canonical Keras-order float32 blob (galvanise_zero_amd/nn/desc.py
+// weight_spec), folds inference BatchNorm (eps 1e-3, model.py:21-22) into the preceding conv,
+// packs conv kernels into bf16 MFMA fragment order and uploads one device allocation.
+#include "forward_kernel.h"
+#include "../../../include/gzero_nn.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace gznn;
+
+static thread_local std::string g_err;
+
+static int fail(const std::string& msg) {
+    g_err = msg;
+    return -1;
+}
+
+#define HIPCHK(x)                                                                        \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+typedef void (*kernel_fn)(KParams, const float*);
+
+struct gz_net {
+    gz_net_desc d;
+    int device = 0;
+    int K0 = 0;
+    size_t nweights = 0;
+    int smem = 0;
+    const void* kfn = nullptr;
+    bool has_weights = false;
+
+    char* dmem = nullptr;          // all weights, one allocation
+    KParams kp{};                  // weight pointers filled in, outputs per launch
+
+    hipStream_t stream = nullptr;  // for the synchronous host-buffer forward
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float* d_io = nullptr;         // staging: planes + outputs
+    int io_cap = 0;
+    float last_ms = 0.f;
+};
+
+extern "C" const char* gz_nn_last_error(void) { return g_err.c_str(); }
+
+// ---- kernel instantiations ----------------------------------------------------------------
+template <int F, int H, int W>
+static const void* kernel_for() {
+    return (const void*)&forward_kernel<F, H, W>;
+}
+
+static const void* select_kernel(int F, int H, int W, int* act_bytes) {
+#define GZ_CASE(F_, H_, W_)                                            \
+    if (F == F_ && H == H_ && W == W_) {                               \
+        *act_bytes = Geo<F_, H_, W_>::ACT_BYTES;                       \
+        return kernel_for<F_, H_, W_>();                               \
+    }
+    GZ_CASE(64, 6, 6)
+    GZ_CASE(128, 6, 6)
+    GZ_CASE(64, 8, 8)
+    GZ_CASE(128, 8, 8)
+#undef GZ_CASE
+    return nullptr;
+}
+
+// ---- bf16 (round to nearest even) -------------------------------------------------------------
+static inline uint16_t f2bf(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+static size_t spec_count(const gz_net_desc& d) {
+    const size_t F = d.cnn_filter_size, C = d.input_channels, k = d.cnn_kernel_size;
+    const size_t HW = (size_t)d.input_columns * d.input_rows;
+    size_t n = k * k * C * F + 4 * F;
+    n += (size_t)d.residual_layers * 2 * (k * k * F * F + 4 * F);
+    for (int r = 0; r < d.role_count; ++r) n += F * 2 + 4 * 2 + 2 * HW * d.policy_dist_count[r] + d.policy_dist_count[r];
+    n += F + HW * d.value_hidden_size + d.value_hidden_size + (size_t)d.value_hidden_size * d.num_values + d.num_values;
+    return n;
+}
+
+extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
+    if (!desc) { fail("null desc"); return nullptr; }
+    const gz_net_desc& d = *desc;
+    if (d.cnn_kernel_size != 3) { fail("only cnn_kernel_size 3 is supported"); return nullptr; }
+    if (d.role_count < 1 || d.role_count > GZ_MAX_ROLES) { fail("role_count out of range"); return nullptr; }
+    if (d.num_values < 1 || d.num_values > 4) { fail("num_values out of range"); return nullptr; }
+    int act_bytes = 0;
+    const void* k = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, &act_bytes);
+    if (!k) {
+        fail("unsupported network geometry F=" + std::to_string(d.cnn_filter_size) + " H=" +
+             std::to_string(d.input_columns) + " W=" + std::to_string(d.input_rows));
+        return nullptr;
+    }
+    gz_net* net = new gz_net;
+    net->d = d;
+    net->device = device;
+    net->kfn = k;
+    net->K0 = ((9 * d.input_channels + 31) / 32) * 32;
+    net->nweights = spec_count(d);
+    int maxP = 0;
+    for (int r = 0; r < d.role_count; ++r) maxP = std::max(maxP, d.policy_dist_count[r]);
+    const int npos = d.input_columns * d.input_rows;
+    net->smem = 2 * act_bytes + scratch_bytes(npos, d.input_channels, net->K0, d.role_count, maxP,
+                                              d.value_hidden_size);
+    KParams& kp = net->kp;
+    kp.C = d.input_channels;
+    kp.K0 = net->K0;
+    kp.B = d.residual_layers;
+    kp.R = d.role_count;
+    kp.VH = d.value_hidden_size;
+    kp.V = d.num_values;
+    kp.leaky = d.leaky_relu;
+    kp.flatten_nchw = d.flatten_nchw;
+    kp.maxP = maxP;
+    for (int r = 0; r < d.role_count; ++r) kp.P[r] = d.policy_dist_count[r];
+
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&net->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&net->ev0) != hipSuccess || hipEventCreate(&net->ev1) != hipSuccess) {
+        fail(std::string("HIP init failed: ") + hipGetErrorString(hipGetLastError()));
+        delete net;
+        return nullptr;
+    }
+    if (net->smem > 64 * 1024) {
+        if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, net->smem) != hipSuccess) {
+            fail("cannot raise dynamic LDS limit");
+            delete net;
+            return nullptr;
+        }
+    }
+    return net;
+}
+
+extern "C" void gz_net_destroy(gz_net* net) {
+    if (!net) return;
+    (void)hipSetDevice(net->device);
+    if (net->dmem) (void)hipFree(net->dmem);
+    if (net->d_io) (void)hipFree(net->d_io);
+    if (net->ev0) (void)hipEventDestroy(net->ev0);
+    if (net->ev1) (void)hipEventDestroy(net->ev1);
+    if (net->stream) (void)hipStreamDestroy(net->stream);
+    delete net;
+}
+
+extern "C" size_t gz_net_weight_count(const gz_net* net) { return net ? net->nweights : 0; }
+
+extern "C" double gz_net_flops_per_eval(const gz_net* net) {
+    const gz_net_desc& d = net->d;
+    const double F = d.cnn_filter_size, C = d.input_channels, HW = (double)d.input_columns * d.input_rows;
+    double f = 2 * HW * C * F * 9 + d.residual_layers * 2 * (2 * HW * F * F * 9);
+    for (int r = 0; r < d.role_count; ++r) f += 2 * HW * F * 2 + 2 * (2 * HW) * d.policy_dist_count[r];
+    f += 2 * HW * F + 2 * HW * d.value_hidden_size + 2.0 * d.value_hidden_size * d.num_values;
+    return f;
+}
+
+// ---- weight folding / packing ---------------------------------------------------------------
+namespace {
+struct Cursor {
+    const float* p;
+    const float* take(size_t n) { const float* r = p; p += n; return r; }
+};
+
+struct Layout {
+    size_t off = 0;
+    size_t alloc(size_t bytes) { size_t o = off; off = (off + bytes + 255) & ~(size_t)255; return o; }
+};
+}  // namespace
+
+extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) {
+    if (!net || !blob) return fail("null argument");
+    if (count != net->nweights)
+        return fail("weight count mismatch: got " + std::to_string(count) + " expected " + std::to_string(net->nweights));
+    const gz_net_desc& d = net->d;
+    const int F = d.cnn_filter_size, C = d.input_channels, B = d.residual_layers, R = d.role_count;
+    const int HW = d.input_columns * d.input_rows, K0 = net->K0, KC = F / 32;
+    const int HC = 2 * R + 1;
+    const float eps = 1e-3f;
+
+    // host images
+    std::vector<uint16_t> w0((size_t)K0 * F, 0);
+    std::vector<float> b0(F);
+    std::vector<uint16_t> wres((size_t)2 * B * 9 * F * F);
+    std::vector<float> bres((size_t)2 * B * F);
+    std::vector<float> wh((size_t)HC * F), bh(HC, 0.f);
+
+    Cursor cur{blob};
+    auto bn_fold = [&](int n, std::vector<float>& scale, std::vector<float>& bias) {
+        const float* g = cur.take(n);
+        const float* be = cur.take(n);
+        const float* mu = cur.take(n);
+        const float* var = cur.take(n);
+        scale.resize(n);
+        bias.resize(n);
+        for (int i = 0; i < n; ++i) {
+            scale[i] = g[i] / std::sqrt(var[i] + eps);
+            bias[i] = be[i] - mu[i] * scale[i];
+        }
+    };
+    std::vector<float> s, bb;
+    {   // initial conv [3][3][C][F] -> w0[kc][co][32], k = tap*C + c
+        const float* w = cur.take((size_t)9 * C * F);
+        bn_fold(F, s, bb);
+        for (int co = 0; co < F; ++co) {
+            b0[co] = bb[co];
+            for (int k = 0; k < 9 * C; ++k) {
+                const int tap = k / C, c = k % C;
+                const float v = w[((size_t)tap * C + c) * F + co] * s[co];
+                w0[((size_t)(k / 32) * F + co) * 32 + (k % 32)] = f2bf(v);
+            }
+        }
+    }
+    for (int conv = 0; conv < 2 * B; ++conv) {  // [3][3][F][F] -> [tap][kc][co][32]
+        const float* w = cur.take((size_t)9 * F * F);
+        bn_fold(F, s, bb);
+        uint16_t* dst = wres.data() + (size_t)conv * 9 * F * F;
+        for (int co = 0; co < F; ++co) {
+            bres[(size_t)conv * F + co] = bb[co];
+            for (int tap = 0; tap < 9; ++tap)
+                for (int ci = 0; ci < F; ++ci) {
+                    const float v = w[((size_t)tap * F + ci) * F + co] * s[co];
+                    dst[(((size_t)tap * KC + ci / 32) * F + co) * 32 + (ci % 32)] = f2bf(v);
+                }
+        }
+    }
+    std::vector<const float*> pdense(R), pbias(R);
+    for (int r = 0; r < R; ++r) {
+        const float* w = cur.take((size_t)F * 2);   // [1][1][F][2]
+        bn_fold(2, s, bb);
+        for (int c = 0; c < 2; ++c) {
+            for (int f = 0; f < F; ++f) wh[(size_t)(2 * r + c) * F + f] = w[(size_t)f * 2 + c] * s[c];
+            bh[2 * r + c] = bb[c];
+        }
+        pdense[r] = cur.take((size_t)2 * HW * d.policy_dist_count[r]);
+        pbias[r] = cur.take(d.policy_dist_count[r]);
+    }
+    {
+        const float* w = cur.take(F);   // [1][1][F][1], no BN, no bias (model.py:275-279)
+        for (int f = 0; f < F; ++f) wh[(size_t)(2 * R) * F + f] = w[f];
+        bh[2 * R] = 0.f;
+    }
+    const float* vhw = cur.take((size_t)HW * d.value_hidden_size);
+    const float* vhb = cur.take(d.value_hidden_size);
+    const float* vdw = cur.take((size_t)d.value_hidden_size * d.num_values);
+    const float* vdb = cur.take(d.num_values);
+    if ((size_t)(cur.p - blob) != count) return fail("internal: blob cursor mismatch");
+
+    // device layout
+    Layout L;
+    const size_t o_w0 = L.alloc(w0.size() * 2), o_b0 = L.alloc(b0.size() * 4);
+    const size_t o_wres = L.alloc(wres.size() * 2), o_bres = L.alloc(bres.size() * 4);
+    const size_t o_wh = L.alloc(wh.size() * 4), o_bh = L.alloc(bh.size() * 4);
+    size_t o_pd[GZ_MAX_ROLES], o_pb[GZ_MAX_ROLES];
+    for (int r = 0; r < R; ++r) {
+        o_pd[r] = L.alloc((size_t)2 * HW * d.policy_dist_count[r] * 4);
+        o_pb[r] = L.alloc((size_t)d.policy_dist_count[r] * 4);
+    }
+    const size_t o_vhw = L.alloc((size_t)HW * d.value_hidden_size * 4), o_vhb = L.alloc(d.value_hidden_size * 4);
+    const size_t o_vdw = L.alloc((size_t)d.value_hidden_size * d.num_values * 4), o_vdb = L.alloc(d.num_values * 4);
+
+    std::vector<char> img(L.off, 0);
+    auto put = [&](size_t off, const void* src, size_t bytes) { std::memcpy(img.data() + off, src, bytes); };
+    put(o_w0, w0.data(), w0.size() * 2);
+    put(o_b0, b0.data(), b0.size() * 4);
+    put(o_wres, wres.data(), wres.size() * 2);
+    put(o_bres, bres.data(), bres.size() * 4);
+    put(o_wh, wh.data(), wh.size() * 4);
+    put(o_bh, bh.data(), bh.size() * 4);
+    for (int r = 0; r < R; ++r) {
+        put(o_pd[r], pdense[r], (size_t)2 * HW * d.policy_dist_count[r] * 4);
+        put(o_pb[r], pbias[r], (size_t)d.policy_dist_count[r] * 4);
+    }
+    put(o_vhw, vhw, (size_t)HW * d.value_hidden_size * 4);
+    put(o_vhb, vhb, d.value_hidden_size * 4);
+    put(o_vdw, vdw, (size_t)d.value_hidden_size * d.num_values * 4);
+    put(o_vdb, vdb, d.num_values * 4);
+
+    HIPCHK(hipSetDevice(net->device));
+    if (net->dmem) { HIPCHK(hipFree(net->dmem)); net->dmem = nullptr; }
+    HIPCHK(hipMalloc((void**)&net->dmem, L.off));
+    HIPCHK(hipMemcpy(net->dmem, img.data(), L.off, hipMemcpyHostToDevice));
+
+    KParams& kp = net->kp;
+    char* m = net->dmem;
+    kp.w0 = (const __bf16*)(m + o_w0);
+    kp.b0 = (const float*)(m + o_b0);
+    kp.wres = (const __bf16*)(m + o_wres);
+    kp.bres = (const float*)(m + o_bres);
+    kp.wh = (const float*)(m + o_wh);
+    kp.bh = (const float*)(m + o_bh);
+    for (int r = 0; r < R; ++r) {
+        kp.pd[r] = (const float*)(m + o_pd[r]);
+        kp.pb[r] = (const float*)(m + o_pb[r]);
+    }
+    kp.vhw = (const float*)(m + o_vhw);
+    kp.vhb = (const float*)(m + o_vhb);
+    kp.vdw = (const float*)(m + o_vdw);
+    kp.vdb = (const float*)(m + o_vdb);
+    net->has_weights = true;
+    return 0;
+}
+
+extern "C" int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_t count) {
+    if (!net || !d_blob) return fail("null argument");
+    std::vector<float> h(count);
+    HIPCHK(hipSetDevice(net->device));
+    HIPCHK(hipMemcpy(h.data(), d_blob, count * 4, hipMemcpyDeviceToHost));
+    return gz_net_set_weights(net, h.data(), count);
+}
+
+static int launch(gz_net* net, hipStream_t stream, const float* d_planes, int n,
+                  float* const* d_pol, float* d_val) {
+    if (!net->has_weights) return fail("weights not set");
+    if (n <= 0) return 0;
+    KParams kp = net->kp;
+    for (int r = 0; r < kp.R; ++r) kp.pol[r] = d_pol[r];
+    kp.val = d_val;
+    void* args[] = {&kp, &d_planes};
+    HIPCHK(hipLaunchKernel(net->kfn, dim3(n), dim3(kThreads), args, net->smem, stream));
+    return 0;
+}
+
+extern "C" int gz_net_forward_device(gz_net* net, void* stream, const float* d_planes, int n,
+                                     float* const* d_policies, float* d_values) {
+    if (!net) return fail("null net");
+    return launch(net, (hipStream_t)stream, d_planes, n, d_policies, d_values);
+}
+
+extern "C" int gz_net_forward(gz_net* net, const float* planes, int n, float* const* policies, float* values) {
+    if (!net || !planes || !policies || !values) return fail("null argument");
+    if (n <= 0) return 0;
+    const gz_net_desc& d = net->d;
+    const size_t in_f = (size_t)d.input_channels * d.input_columns * d.input_rows;
+    size_t out_f = d.num_values;
+    for (int r = 0; r < d.role_count; ++r) out_f += d.policy_dist_count[r];
+    HIPCHK(hipSetDevice(net->device));
+    if (n > net->io_cap) {
+        if (net->d_io) HIPCHK(hipFree(net->d_io));
+        net->d_io = nullptr;
+        HIPCHK(hipMalloc((void**)&net->d_io, (size_t)n * (in_f + out_f) * 4 + 1024));
+        net->io_cap = n;
+    }
+    float* d_in = net->d_io;
+    float* d_pol[GZ_MAX_ROLES];
+    float* p = d_in + (size_t)n * in_f;
+    for (int r = 0; r < d.role_count; ++r) { d_pol[r] = p; p += (size_t)n * d.policy_dist_count[r]; }
+    float* d_val = p;
+    HIPCHK(hipMemcpyAsync(d_in, planes, (size_t)n * in_f * 4, hipMemcpyHostToDevice, net->stream));
+    HIPCHK(hipEventRecord(net->ev0, net->stream));
+    if (launch(net, net->stream, d_in, n, d_pol, d_val)) return -1;
+    HIPCHK(hipEventRecord(net->ev1, net->stream));
+    for (int r = 0; r < d.role_count; ++r)
+        HIPCHK(hipMemcpyAsync(policies[r], d_pol[r], (size_t)n * d.policy_dist_count[r] * 4, hipMemcpyDeviceToHost, net->stream));
+    HIPCHK(hipMemcpyAsync(values, d_val, (size_t)n * d.num_values * 4, hipMemcpyDeviceToHost, net->stream));
+    HIPCHK(hipStreamSynchronize(net->stream));
+    HIPCHK(hipEventElapsedTime(&net->last_ms, net->ev0, net->ev1));
+    return 0;
+}
+
+extern "C" float gz_net_last_kernel_ms(const gz_net* net) { return net ? net->last_ms : 0.f; }

@@ -1,0 +1,112 @@
+"""Network description + canonical weight-blob layout for the v1 (AlphaGo-Zero style) residual CNN.
+
+Restates the topology built by ``get_network_model`` (reference ``src/ggpzero/nn/model.py:154-296``)
+for the ``resnet_v2=False`` path, which is the one every BASELINE config uses:
+
+* initial ``conv2d_block(F, k, use_bias=False) -> BN -> act``            (model.py:205-208, 25-44)
+* ``residual_layers`` x ``residual_block_v1``: conv-BN-act-conv-BN-add-act (model.py:47-75)
+* per role: ``conv2d_block(2, 1)`` -> BN -> act -> Flatten -> Dense(P_r, softmax)  (model.py:223-241)
+* value:  ``conv2d_block(1, 1, do_bn=False)`` -> act -> Flatten -> Dense(hidden, act)
+  -> Dense(V, softmax)                                                     (model.py:273-291)
+
+BatchNormalization is inference-mode with epsilon 1e-3 (Keras default; every
+``data/*/models/*.json`` records ``epsilon: 0.001``).
+
+The canonical blob is the concatenation, in the order of :func:`weight_spec`, of float32 tensors in
+Keras storage layout (conv kernels HWIO ``[kh][kw][cin][cout]``, dense ``[in][out]``).  This is the
+order a Keras ``model.get_weights()`` of the reference model produces once the BN tensors are
+grouped as (gamma, beta, moving_mean, moving_variance).  The C-ABI ``gz_net_set_weights``
+(``include/gzero_nn.h``) consumes exactly this blob.
+"""
+
+from dataclasses import dataclass, field
+from typing import List, Tuple
+
+BN_EPSILON = 1e-3
+LEAKY_ALPHA = 0.03          # klayers.LeakyReLU(alpha=0.03), model.py:13
+
+
+@dataclass
+class NetDesc:
+    """Mirror of the fields of ``confs.NNModelConfig`` (confs.py:127-151) the forward needs."""
+    input_channels: int
+    input_columns: int          # H = len(y_cords)  (bases.py:115-121)
+    input_rows: int             # W = len(x_cords)
+    cnn_filter_size: int
+    residual_layers: int
+    policy_dist_count: List[int]
+    value_hidden_size: int = 256
+    num_values: int = 2         # 3 with a draw head (model.py:246-249)
+    cnn_kernel_size: int = 3
+    leaky_relu: bool = False
+    # Keras >= 2.1.6 Flatten under channels_first permutes to (H, W, C) before flattening; the
+    # legacy (keras 2.1.3) model files flatten in (C, H, W) order.  See SURVEY appendix A.
+    flatten_nchw: bool = False
+
+    @property
+    def role_count(self):
+        return len(self.policy_dist_count)
+
+    @property
+    def hw(self):
+        return self.input_columns * self.input_rows
+
+    def flops_per_eval(self):
+        """Algorithmic FLOPs (2/MAC) of one leaf evaluation, BN/act/softmax excluded."""
+        F, C, HW, k = self.cnn_filter_size, self.input_channels, self.hw, self.cnn_kernel_size
+        f = 2 * HW * C * F * k * k
+        f += self.residual_layers * 2 * (2 * HW * F * F * k * k)
+        for p in self.policy_dist_count:
+            f += 2 * HW * F * 2 + 2 * (2 * HW) * p
+        f += 2 * HW * F + 2 * HW * self.value_hidden_size + 2 * self.value_hidden_size * self.num_values
+        return f
+
+
+def weight_spec(d: NetDesc) -> List[Tuple[str, Tuple[int, ...]]]:
+    """Ordered (name, shape) list of the canonical float32 weight blob."""
+    F, C, k = d.cnn_filter_size, d.input_channels, d.cnn_kernel_size
+    spec = []
+
+    def bn(prefix, n):
+        spec.extend([(prefix + "_gamma", (n,)), (prefix + "_beta", (n,)),
+                     (prefix + "_mean", (n,)), (prefix + "_var", (n,))])
+
+    spec.append(("initial_conv", (k, k, C, F)))
+    bn("initial_bn", F)
+    for i in range(d.residual_layers):
+        spec.append(("res%d_conv0" % i, (k, k, F, F)))
+        bn("res%d_bn0" % i, F)
+        spec.append(("res%d_conv1" % i, (k, k, F, F)))
+        bn("res%d_bn1" % i, F)
+    for r, p in enumerate(d.policy_dist_count):
+        spec.append(("policy%d_conv" % r, (1, 1, F, 2)))
+        bn("policy%d_bn" % r, 2)
+        spec.append(("policy%d_dense" % r, (2 * d.hw, p)))
+        spec.append(("policy%d_bias" % r, (p,)))
+    spec.append(("value_conv", (1, 1, F, 1)))
+    spec.append(("value_hidden", (d.hw, d.value_hidden_size)))
+    spec.append(("value_hidden_bias", (d.value_hidden_size,)))
+    spec.append(("value_dense", (d.value_hidden_size, d.num_values)))
+    spec.append(("value_bias", (d.num_values,)))
+    return spec
+
+
+def blob_size(d: NetDesc) -> int:
+    n = 0
+    for _, shape in weight_spec(d):
+        c = 1
+        for s in shape:
+            c *= s
+        n += c
+    return n
+
+
+# BASELINE.json configs.  C, P_r from the reference model JSONs with
+# num_previous_states=1; net sizes from BASELINE.json.
+BASELINE_CONFIGS = {
+    1: dict(game="breakthroughSmall", desc=NetDesc(5, 6, 6, 64, 2, [81, 81]), evals=100),
+    2: dict(game="breakthrough", desc=NetDesc(5, 8, 8, 128, 6, [155, 155]), evals=800, batch=256),
+    3: dict(game="reversi", desc=NetDesc(5, 8, 8, 128, 10, [65, 65], num_values=3), evals=800),
+    4: dict(game="hexLG13", desc=NetDesc(5, 13, 13, 256, 12, [170, 171]), evals=1600),
+    5: dict(game="amazons_10x10", desc=NetDesc(12, 10, 10, 256, 20, [3041, 3041]), evals=1600),
+}

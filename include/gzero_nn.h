@@ -1,0 +1,78 @@
+/* gzero_nn.h -- C-ABI of the MI355X policy/value network forward (libgz_nn.so).
+ *
+ * Replaces, for the self-play hot path, the Keras model the reference runs through
+ *   NeuralNetwork.get_model().predict_on_batch(X)      src/ggpzero/util/cppinterface.py:119
+ * built by get_network_model()                          src/ggpzero/nn/model.py:154-296 (v1 path)
+ * and loaded by Manager.load_network / create_new_network   src/ggpzero/nn/manager.py:96-139.
+ *
+ * All entry points take plain pointers and sizes.  Every function returning int returns 0 on
+ * success and a negative code on failure; gz_nn_last_error() then holds a message (thread-local).
+ */
+#ifndef GZERO_NN_H
+#define GZERO_NN_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GZ_MAX_ROLES 4
+
+/* Mirror of the forward-relevant fields of confs.NNModelConfig (src/ggpzero/defs/confs.py:127-151)
+ * plus GenerationDescription.draw_head (num_values 3) and the Flatten data_format of the model
+ * file. */
+typedef struct gz_net_desc {
+    int input_channels;                       /* C                                  */
+    int input_columns;                        /* H = len(y_cords)  (bases.py:115)   */
+    int input_rows;                           /* W = len(x_cords)  (bases.py:111)   */
+    int cnn_filter_size;                      /* F                                  */
+    int cnn_kernel_size;                      /* must be 3                          */
+    int residual_layers;                      /* B                                  */
+    int role_count;                           /* R = number of policy heads         */
+    int policy_dist_count[GZ_MAX_ROLES];      /* P_r                                */
+    int value_hidden_size;
+    int num_values;                           /* 2, or 3 with a draw head           */
+    int leaky_relu;                           /* 0: relu, 1: LeakyReLU(alpha=0.03)  */
+    int flatten_nchw;                         /* 0: Keras>=2.1.6 (H,W,C) flatten; 1: legacy (C,H,W) */
+} gz_net_desc;
+
+typedef struct gz_net gz_net;
+
+/* Create a network on HIP device `device`.  Returns NULL on error (see gz_nn_last_error). */
+gz_net* gz_net_create(const gz_net_desc* desc, int device);
+void gz_net_destroy(gz_net* net);
+
+/* Number of float32 values of the canonical weight blob (layout: galvanise_zero_amd/nn/desc.py
+ * weight_spec(): Keras storage order, conv HWIO, BN as gamma,beta,mean,var, dense [in][out]). */
+size_t gz_net_weight_count(const gz_net* net);
+
+/* Upload weights from a host float32 blob (BN folded + packed to bf16 on the host). */
+int gz_net_set_weights(gz_net* net, const float* blob, size_t count);
+
+/* Upload weights from a *device* float32 blob (e.g. after an RCCL broadcast into device memory). */
+int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_t count);
+
+/* Synchronous forward, host buffers: planes float32 [n][C][H][W] (the poll() buffer layout,
+ * cppinterface.py:114); policies[r] float32 [n][P_r]; values float32 [n][num_values].
+ * Equivalent of predict_on_batch on one batch. */
+int gz_net_forward(gz_net* net, const float* planes, int n,
+                   float* const* policies, float* values);
+
+/* Asynchronous forward on a caller stream (hipStream_t passed as void*), device buffers. */
+int gz_net_forward_device(gz_net* net, void* stream, const float* d_planes, int n,
+                          float* const* d_policies, float* d_values);
+
+/* Device time (ms) of the last gz_net_forward kernel, measured with HIP events on its stream. */
+float gz_net_last_kernel_ms(const gz_net* net);
+
+/* Algorithmic FLOPs of one leaf evaluation (2 FLOP/MAC). */
+double gz_net_flops_per_eval(const gz_net* net);
+
+const char* gz_nn_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GZERO_NN_H */

@@ -1,0 +1,137 @@
+"""ORACLE (test infrastructure only) -- CPU restatement of the reference policy/value CNN forward.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module; the
+product path (galvanise_zero_amd) never does.
+
+Restates ``get_network_model`` (reference ``src/ggpzero/nn/model.py:154-296``, v1 / AG0 path) as
+executed by Keras 2.2 / TF 1.12 ``predict_on_batch`` (``src/ggpzero/util/cppinterface.py:119``):
+
+* ``conv2d_block``  model.py:25-44  -- Conv2D(use_bias=False, padding same) -> BatchNormalization
+  (axis=1, inference: gamma*(x-mean)/sqrt(var+eps)+beta, eps=1e-3) -> activation
+* ``residual_block_v1`` model.py:47-75 -- conv-BN-act-conv-BN, add(tensor, x), act
+* policy heads model.py:223-241 -- conv1x1(2)+BN+act, Flatten, Dense(P_r) softmax
+* value head model.py:273-291 -- conv1x1(1) do_bn=False + act, Flatten, Dense(hidden)+act,
+  Dense(V) softmax
+* Flatten: channels_first data in Keras >= 2.1.6 is permuted to (H, W, C) before flattening
+  (``flatten_nchw=False``); legacy files flatten (C, H, W).
+
+Arithmetic is float64 (the fp32 TF result is within ~1e-6 of it); outputs are float32 like
+``predict_on_batch``.  Parity of the reference NN itself is *unpinned*: no reference test holds a
+numeric NN output and the trained weights are absent.
+"""
+
+import numpy as np
+
+EPS = 1e-3
+LEAKY = 0.03
+
+
+def _act(x, leaky):
+    if leaky:
+        return np.where(x > 0, x, LEAKY * x)
+    return np.maximum(x, 0.0)
+
+
+def _bn(x, w, prefix):
+    g, b, m, v = (w[prefix + s].astype(np.float64) for s in ("_gamma", "_beta", "_mean", "_var"))
+    return g * (x - m) / np.sqrt(v + EPS) + b
+
+
+def _conv_same(x, k):
+    """x: [N, H, W, Cin] float64; k: [kh, kw, Cin, Cout] (Keras HWIO), 'same' padding, no bias."""
+    kh, kw = k.shape[0], k.shape[1]
+    ph, pw = kh // 2, kw // 2
+    N, H, W, _ = x.shape
+    xp = np.pad(x, ((0, 0), (ph, ph), (pw, pw), (0, 0)))
+    out = np.zeros((N, H, W, k.shape[3]))
+    for dy in range(kh):
+        for dx in range(kw):
+            out += xp[:, dy:dy + H, dx:dx + W, :] @ k[dy, dx].astype(np.float64)
+    return out
+
+
+def _softmax(z):
+    z = z - z.max(axis=1, keepdims=True)
+    e = np.exp(z)
+    return e / e.sum(axis=1, keepdims=True)
+
+
+def _flatten(x, nchw):
+    # x: [N, H, W, C]
+    if nchw:
+        x = np.transpose(x, (0, 3, 1, 2))
+    return x.reshape(x.shape[0], -1)
+
+
+def forward(desc, weights, planes):
+    """planes: float32 [N, C, H, W] (the poll() layout, cppinterface.py:114).
+
+    Returns [policy_0 [N,P_0], ..., policy_{R-1}, value [N,V]] float32 (model.py:294 order)."""
+    w = dict(weights)
+    leaky = desc.leaky_relu
+    x = np.transpose(planes.astype(np.float64), (0, 2, 3, 1))     # NHWC
+    x = _act(_bn(_conv_same(x, w["initial_conv"]), w, "initial_bn"), leaky)
+    for i in range(desc.residual_layers):
+        t = x
+        y = _act(_bn(_conv_same(x, w["res%d_conv0" % i]), w, "res%d_bn0" % i), leaky)
+        y = _bn(_conv_same(y, w["res%d_conv1" % i]), w, "res%d_bn1" % i)
+        x = _act(t + y, leaky)
+    outs = []
+    for r in range(desc.role_count):
+        h = _act(_bn(_conv_same(x, w["policy%d_conv" % r]), w, "policy%d_bn" % r), leaky)
+        logits = _flatten(h, desc.flatten_nchw) @ w["policy%d_dense" % r].astype(np.float64)
+        logits = logits + w["policy%d_bias" % r]
+        outs.append(_softmax(logits).astype(np.float32))
+    v = _act(_conv_same(x, w["value_conv"]), leaky)
+    hid = _act(_flatten(v, desc.flatten_nchw) @ w["value_hidden"].astype(np.float64)
+               + w["value_hidden_bias"], leaky)
+    val = hid @ w["value_dense"].astype(np.float64) + w["value_bias"]
+    outs.append(_softmax(val).astype(np.float32))
+    return outs
+
+
+# ---------------------------------------------------------------------------------------------
+# bf16-emulating variant: same math as the HIP kernel's numerics contract (BN folded into the
+# conv in float32, folded conv weights and conv *inputs* rounded to bf16 RNE, float accumulate,
+# residual stream and heads in full precision).  Used to test the kernel tightly; the float64
+# forward() above is the reference semantics the stated tolerance is measured against.
+
+def bf16_round(a):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    u = a.view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+    return (u.astype(np.uint32) << 16).view(np.float32)
+
+
+def _fold(w, conv, bn):
+    k = w[conv].astype(np.float32)
+    g, b, m, v = (w[bn + s].astype(np.float32) for s in ("_gamma", "_beta", "_mean", "_var"))
+    s = g / np.sqrt(v + np.float32(EPS))
+    return (k * s).astype(np.float32), (b - m * s).astype(np.float32)
+
+
+def forward_bf16_emulated(desc, weights, planes):
+    w = dict(weights)
+    leaky = desc.leaky_relu
+    x = bf16_round(np.transpose(planes, (0, 2, 3, 1))).astype(np.float64)
+    k, b = _fold(w, "initial_conv", "initial_bn")
+    x = _act(_conv_same(x, bf16_round(k)) + b, leaky)
+    for i in range(desc.residual_layers):
+        t = x
+        k0, b0 = _fold(w, "res%d_conv0" % i, "res%d_bn0" % i)
+        k1, b1 = _fold(w, "res%d_conv1" % i, "res%d_bn1" % i)
+        y = _act(_conv_same(bf16_round(x).astype(np.float64), bf16_round(k0)) + b0, leaky)
+        y = _conv_same(bf16_round(y).astype(np.float64), bf16_round(k1)) + b1
+        x = _act(t + y, leaky)
+    outs = []
+    for r in range(desc.role_count):
+        k, b = _fold(w, "policy%d_conv" % r, "policy%d_bn" % r)
+        h = _act(_conv_same(x, k) + b, leaky)
+        logits = _flatten(h, desc.flatten_nchw) @ w["policy%d_dense" % r].astype(np.float64)
+        outs.append(_softmax(logits + w["policy%d_bias" % r]).astype(np.float32))
+    v = _act(_conv_same(x, w["value_conv"]), leaky)
+    hid = _act(_flatten(v, desc.flatten_nchw) @ w["value_hidden"].astype(np.float64)
+               + w["value_hidden_bias"], leaky)
+    val = hid @ w["value_dense"].astype(np.float64) + w["value_bias"]
+    outs.append(_softmax(val).astype(np.float32))
+    return outs

@@ -1,0 +1,93 @@
+"""GPU parity of the fused HIP forward (libgz_nn.so via its C-ABI) against the oracle.
+
+Stated tolerance (bf16 MFMA operands, fp32 accumulate, fp32 residual stream and heads), measured
+against the float64 reference semantics oracle/nn_ref.forward:
+    policies / values: max |err| <= 5e-2, mean |err| <= 1e-3     (TOL_REF)
+and against the bf16-emulating oracle (same rounding points as the kernel, differing only in
+accumulation order):
+    max |err| <= 1e-2, mean |err| <= 5e-5                        (TOL_EMU)
+Row results must be bit-identical regardless of batch size / slot (batch invariance, needed for
+bit-exact PUCT visit counts under batching).
+"""
+import numpy as np
+import pytest
+
+from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS, NetDesc
+from galvanise_zero_amd.nn.weights import random_planes, random_weights, to_blob
+from oracle import nn_ref
+
+TOL_REF = (5e-2, 1e-3)
+TOL_EMU = (1e-2, 5e-5)
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = {
+    "cfg1": BASELINE_CONFIGS[1]["desc"],
+    "cfg2": BASELINE_CONFIGS[2]["desc"],
+    "b0_8x8": NetDesc(5, 8, 8, 128, 0, [155, 155]),
+    "leaky_v3_8x8": NetDesc(5, 8, 8, 64, 1, [65, 65], num_values=3, leaky_relu=True),
+    "nchw_6x6": NetDesc(5, 6, 6, 128, 1, [81, 81], flatten_nchw=True),
+}
+
+
+def _net(desc, seed, device):
+    from galvanise_zero_amd._native import HipNet
+    w = random_weights(desc, seed, bias_std=0.2)
+    net = HipNet(desc, device)
+    net.set_weights(to_blob(w))
+    return net, w
+
+
+def _err(a, b):
+    d = np.abs(a.astype(np.float64) - b.astype(np.float64))
+    return float(d.max()), float(d.mean())
+
+
+@pytest.mark.parametrize("name", list(VARIANTS))
+def test_forward_parity(name, hip_device):
+    desc = VARIANTS[name]
+    net, w = _net(desc, 7919, hip_device)
+    for n in (1, 7, 64):
+        x = random_planes(desc, n, 100 + n)
+        got = net.forward(x)
+        ref = nn_ref.forward(desc, w, x)
+        emu = nn_ref.forward_bf16_emulated(desc, w, x)
+        for i, (g, r, e) in enumerate(zip(got, ref, emu)):
+            assert g.shape == r.shape
+            assert np.all(np.isfinite(g))
+            er, ee = _err(g, r), _err(g, e)
+            print("%s n=%d out%d  vs_ref max %.3g mean %.3g | vs_emu max %.3g mean %.3g"
+                  % (name, n, i, er[0], er[1], ee[0], ee[1]))
+            assert er[0] <= TOL_REF[0] and er[1] <= TOL_REF[1], (name, n, i, er)
+            assert ee[0] <= TOL_EMU[0] and ee[1] <= TOL_EMU[1], (name, n, i, ee)
+            np.testing.assert_allclose(g.sum(axis=1), 1.0, atol=1e-4)
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2"])
+def test_batch_invariance(name, hip_device):
+    desc = VARIANTS[name]
+    net, _ = _net(desc, 3, hip_device)
+    x = random_planes(desc, 256, 9)
+    full = net.forward(x)
+    # same rows in a different batch composition / slot
+    perm = np.random.default_rng(0).permutation(256)[:37]
+    part = net.forward(x[perm])
+    for a, b in zip(full, part):
+        assert np.array_equal(a[perm], b)
+    single = net.forward(x[5:6])
+    for a, b in zip(full, single):
+        assert np.array_equal(a[5:6], b)
+
+
+def test_large_batch_and_timing(hip_device):
+    desc = VARIANTS["cfg2"]
+    net, w = _net(desc, 1, hip_device)
+    x = random_planes(desc, 1024, 5)
+    got = net.forward(x)
+    ref = nn_ref.forward(desc, w, x[:16])
+    for g, r in zip(got, ref):
+        assert _err(g[:16], r)[0] <= TOL_REF[0]
+    ms = net.last_kernel_ms()
+    tflops = desc.flops_per_eval() * 1024 / (ms * 1e-3) / 1e12
+    print("cfg2 N=1024 kernel %.3f ms  %.1f TFLOP/s" % (ms, tflops))
+    assert ms > 0
