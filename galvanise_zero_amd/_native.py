@@ -163,3 +163,188 @@ class HipNet(object):
             self.close()
         except Exception:
             pass
+
+
+###############################################################################
+# libgz_engine.so
+
+class GzPuctConfig(ctypes.Structure):
+    _fields_ = [("verbose", ctypes.c_int),
+                ("puct_constant", ctypes.c_float),
+                ("puct_constant_root", ctypes.c_float),
+                ("dirichlet_noise_pct", ctypes.c_float),
+                ("noise_policy_squash_pct", ctypes.c_float),
+                ("noise_policy_squash_prob", ctypes.c_float),
+                ("choose", ctypes.c_int),
+                ("max_dump_depth", ctypes.c_int),
+                ("random_scale", ctypes.c_float),
+                ("temperature", ctypes.c_float),
+                ("depth_temperature_start", ctypes.c_int),
+                ("depth_temperature_increment", ctypes.c_float),
+                ("depth_temperature_stop", ctypes.c_int),
+                ("depth_temperature_max", ctypes.c_float),
+                ("fpu_prior_discount", ctypes.c_float),
+                ("fpu_prior_discount_root", ctypes.c_float),
+                ("top_visits_best_guess_converge_ratio", ctypes.c_float),
+                ("think_time", ctypes.c_float),
+                ("converged_visits", ctypes.c_int),
+                ("batch_size", ctypes.c_int),
+                ("use_legals_count_draw", ctypes.c_int),
+                ("backup_finalised", ctypes.c_int),
+                ("lookup_transpositions", ctypes.c_int),
+                ("evaluation_multiplier_to_convergence", ctypes.c_float)]
+
+
+class GzSelfPlayConfig(ctypes.Structure):
+    _fields_ = [("oscillate_sampling_pct", ctypes.c_float),
+                ("temperature_for_policy", ctypes.c_float),
+                ("puct_config", GzPuctConfig),
+                ("evals_per_move", ctypes.c_int),
+                ("resign0_score_probability", ctypes.c_float),
+                ("resign0_pct", ctypes.c_float),
+                ("resign1_score_probability", ctypes.c_float),
+                ("resign1_pct", ctypes.c_float),
+                ("abort_max_length", ctypes.c_int),
+                ("number_repeat_states_draw", ctypes.c_int),
+                ("repeat_states_score", ctypes.c_float),
+                ("run_to_end_pct", ctypes.c_float),
+                ("run_to_end_evals", ctypes.c_int),
+                ("run_to_end_puct_config", GzPuctConfig),
+                ("run_to_end_early_score", ctypes.c_float),
+                ("run_to_end_minimum_game_depth", ctypes.c_int)]
+
+
+class GzPoolStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_long) for n in (
+        "games_started", "games_completed", "games_with_samples", "samples", "no_samples", "dupes",
+        "resigns", "false_positive_resigns0", "false_positive_resigns1", "early_run_to_ends",
+        "aborts_game_length", "evaluations", "polls")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_VP = ctypes.c_void_p
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+_IP = ctypes.POINTER(ctypes.c_int)
+
+_ENGINE_SIGS = {
+    "gz_engine_last_error": (ctypes.c_char_p, []),
+    "gz_free": (None, [_VP]),
+    "gz_sm_create": (_VP, [ctypes.c_char_p]),
+    "gz_sm_destroy": (None, [_VP]),
+    "gz_sm_role_count": (ctypes.c_int, [_VP]),
+    "gz_sm_num_bases": (ctypes.c_int, [_VP]),
+    "gz_sm_num_words": (ctypes.c_int, [_VP]),
+    "gz_sm_action_count": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "gz_sm_base_name": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    "gz_sm_role_name": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    "gz_sm_legal_to_move": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    "gz_sm_initial_state": (ctypes.c_int, [_VP, _U64P]),
+    "gz_sm_update_bases": (ctypes.c_int, [_VP, _U64P]),
+    "gz_sm_legal_count": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "gz_sm_legal": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int]),
+    "gz_sm_is_terminal": (ctypes.c_int, [_VP]),
+    "gz_sm_goal_value": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "gz_sm_next_state": (ctypes.c_int, [_VP, _IP, _U64P]),
+    "gz_transformer_create": (_VP, [ctypes.c_int] * 5 + [_IP, ctypes.c_int]),
+    "gz_transformer_destroy": (None, [_VP]),
+    "gz_transformer_add_board_base": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int]),
+    "gz_transformer_add_control_base": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_float]),
+    "gz_transformer_total_size": (ctypes.c_int, [_VP]),
+    "gz_transformer_to_channels": (ctypes.c_int, [_VP, _U64P, ctypes.POINTER(_U64P), ctypes.c_int, _FP]),
+    "gz_supervisor_create": (_VP, [_VP, _VP, ctypes.c_int, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int]),
+    "gz_supervisor_destroy": (None, [_VP]),
+    "gz_supervisor_start_self_play": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.POINTER(GzSelfPlayConfig)]),
+    "gz_supervisor_poll": (_FP, [_VP, ctypes.c_int, ctypes.POINTER(_FP), ctypes.c_int, _IP]),
+    "gz_supervisor_fetch_samples": (_VP, [_VP]),
+    "gz_supervisor_add_unique_state": (ctypes.c_int, [_VP, _U64P]),
+    "gz_supervisor_clear_unique_states": (ctypes.c_int, [_VP]),
+    "gz_supervisor_stats": (ctypes.c_int, [_VP, ctypes.POINTER(GzPoolStats)]),
+    "gz_supervisor_set_sample_interval": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "gz_player_create": (_VP, [_VP, _VP, ctypes.POINTER(GzPuctConfig), ctypes.c_uint64]),
+    "gz_player_destroy": (None, [_VP]),
+    "gz_player_reset": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "gz_player_apply_move": (ctypes.c_int, [_VP, _IP]),
+    "gz_player_move": (ctypes.c_int, [_VP, _U64P, ctypes.c_int, ctypes.c_double]),
+    "gz_player_get_move": (ctypes.c_int, [_VP, ctypes.c_int, _IP, _FP, _IP]),
+    "gz_player_update_config": (ctypes.c_int, [_VP, ctypes.c_double, ctypes.c_int, ctypes.c_int]),
+    "gz_player_balance_moves": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "gz_player_tree_debug": (_VP, [_VP, ctypes.c_int]),
+    "gz_player_poll": (_FP, [_VP, ctypes.c_int, ctypes.POINTER(_FP), ctypes.c_int, _IP]),
+    "gz_player_root_children": (ctypes.c_int, [_VP, _IP, ctypes.POINTER(ctypes.c_uint32), _FP, ctypes.c_int]),
+    "gz_unique_states_create": (_VP, [_VP, _VP, ctypes.c_int]),
+    "gz_unique_states_destroy": (None, [_VP]),
+    "gz_pool_create": (_VP, [_VP, _VP, ctypes.c_int, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_long, _VP,
+                             _FP, ctypes.POINTER(_FP), _FP]),
+    "gz_pool_destroy": (None, [_VP]),
+    "gz_pool_start": (ctypes.c_int, [_VP, ctypes.POINTER(GzSelfPlayConfig)]),
+    "gz_pool_poll": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "gz_pool_get_stats": (ctypes.c_int, [_VP, ctypes.POINTER(GzPoolStats)]),
+    "gz_pool_fetch_samples": (_VP, [_VP]),
+    "gz_pool_take_sample_count": (ctypes.c_long, [_VP]),
+}
+
+
+def engine_lib():
+    lib = _load("libgz_engine.so")
+    if not getattr(lib, "_gz_typed", False):
+        for name, (res, args) in _ENGINE_SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        lib._gz_typed = True
+    return lib
+
+
+def engine_error():
+    return engine_lib().gz_engine_last_error().decode()
+
+
+def take_string(ptr):
+    """Copy and free a malloc'd C string returned by the engine (None for NULL)."""
+    if not ptr:
+        return None
+    s = ctypes.string_at(ptr).decode()
+    engine_lib().gz_free(ptr)
+    return s
+
+
+_CHOOSE = {"choose_top_visits": 0, "choose_temperature": 1}
+
+
+def _get(conf, name, default):
+    """Read a config field from an attrs record or a dict; missing keys keep the default (the
+    reference's createSelfPlayConfig reads keys Python never sets, common.cpp:154-155)."""
+    if isinstance(conf, dict):
+        return conf.get(name, default)
+    return getattr(conf, name, default)
+
+
+def make_puct_config(conf):
+    from .defs import confs
+    d = confs.PUCTEvaluatorConfig()
+    c = GzPuctConfig()
+    for name, ctype in GzPuctConfig._fields_:
+        v = _get(conf, name, getattr(d, name))
+        if name == "choose":
+            if isinstance(v, str):
+                v = _CHOOSE.get(v, 0)
+        setattr(c, name, int(v) if ctype is ctypes.c_int else float(v))
+    return c
+
+
+def make_selfplay_config(conf):
+    from .defs import confs
+    d = confs.SelfPlayConfig()
+    c = GzSelfPlayConfig()
+    for name, ctype in GzSelfPlayConfig._fields_:
+        if name in ("puct_config", "run_to_end_puct_config"):
+            setattr(c, name, make_puct_config(_get(conf, name, getattr(d, name))))
+            continue
+        default = {"number_repeat_states_draw": -1, "repeat_states_score": 0.5}.get(name)
+        if default is None:
+            default = getattr(d, name)
+        v = _get(conf, name, default)
+        setattr(c, name, int(v) if ctype is ctypes.c_int else float(v))
+    return c

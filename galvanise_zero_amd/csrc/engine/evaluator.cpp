@@ -1,0 +1,767 @@
+// Restatement of src/cpp/puct/evaluator.cpp.  Float/double mixing follows the reference
+// expression by expression (e.g. selectChild's double `score` against float `best_score`), and the
+// library is compiled with -ffp-contract=off so every operation rounds as written (the reference's
+// contraction behaviour depends on its unknown k273 build flags and is unpinned).
+#include "evaluator.h"
+
+#include "transformer.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <limits>
+#include <random>
+
+namespace gz {
+
+#define GZ_ASSERT(cond)                                                                     \
+    do {                                                                                    \
+        if (!(cond)) {                                                                      \
+            std::fprintf(stderr, "gz assertion failed: %s (%s:%d)\n", #cond, __FILE__, __LINE__); \
+            std::abort();                                                                   \
+        }                                                                                   \
+    } while (0)
+
+double get_time() {
+    using namespace std::chrono;
+    return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+size_t PuctEvaluator::MaskedHash::operator()(const MaskedKey& k) const {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (uint64_t w : k.w) {
+        h ^= w + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    }
+    return (size_t)h;
+}
+
+PuctEvaluator::MaskedKey PuctEvaluator::maskedKey(const uint64_t* bs) const {
+    MaskedKey k;
+    k.w.resize(hash_mask.size());
+    for (size_t i = 0; i < hash_mask.size(); ++i) k.w[i] = bs[i] & hash_mask[i];
+    return k;
+}
+
+PuctEvaluator::PuctEvaluator(StateMachine* sm, NetworkScheduler* scheduler, const GdlBasesTransformer* transformer)
+    : sm(sm), scheduler(scheduler) {
+    basestate_expand_node.assign(sm->numWords(), 0);
+    hash_mask = transformer->createHashMask(sm->numBases());
+}
+
+PuctEvaluator::~PuctEvaluator() { reset(0); }
+
+void PuctEvaluator::updateConf(const PuctConfig* c) { conf = c; }
+
+// evaluator.cpp:102-140
+void PuctEvaluator::removeNode(PuctNode* node) {
+    if (conf->lookup_transpositions) lookup.erase(maskedKey(node->getBaseState()));
+    node_allocated_memory -= node->allocated_size;
+    PuctNode::destroy(node);
+    number_of_nodes--;
+}
+
+void PuctEvaluator::releaseNodes(PuctNode* current) {
+    const int role_count = sm->roleCount();
+    for (int ii = 0; ii < current->num_children; ii++) {
+        PuctNodeChild* child = current->getNodeChild(role_count, ii);
+        if (child->to_node != nullptr) {
+            PuctNode* next_node = child->to_node;
+            if (next_node->ref_count <= 0) continue;   // cycle guard
+            child->to_node = nullptr;
+            next_node->ref_count--;
+            if (next_node->ref_count == 0) {
+                releaseNodes(next_node);
+                garbage.push_back(next_node);
+            }
+        }
+    }
+}
+
+// evaluator.cpp:144-163
+PuctNode* PuctEvaluator::lookupNode(const uint64_t* bs, int depth) {
+    if (!conf->lookup_transpositions) return nullptr;
+    auto found = lookup.find(maskedKey(bs));
+    if (found != lookup.end()) {
+        PuctNode* result = found->second;
+        if (result->game_depth != depth) return nullptr;
+        return result;
+    }
+    return nullptr;
+}
+
+// evaluator.cpp:165-214
+PuctNode* PuctEvaluator::createNode(PuctNode* parent, const uint64_t* state) {
+    PuctNode* new_node = PuctNode::create(state, sm);
+    if (conf->lookup_transpositions) lookup.emplace(maskedKey(new_node->getBaseState()), new_node);
+    number_of_nodes++;
+    node_allocated_memory += new_node->allocated_size;
+
+    new_node->parent = parent;
+    if (parent != nullptr) {
+        new_node->game_depth = parent->game_depth + 1;
+        parent->num_children_expanded++;
+    } else {
+        new_node->game_depth = game_depth;
+    }
+
+    if (new_node->is_finalised) {
+        for (int ii = 0; ii < sm->roleCount(); ii++) {
+            const float s = new_node->getCurrentScore(ii);
+            if (s > 0.99) new_node->setCurrentScore(ii, s * 1.05);
+            else if (s < 0.01) new_node->setCurrentScore(ii, -0.05);
+        }
+        return new_node;
+    }
+
+    if (new_node->num_children == 1) return new_node;
+
+    PuctNodeRequest req(new_node);
+    scheduler->evaluate(&req);
+    stats.num_evaluations++;
+    total_evaluations++;
+    return new_node;
+}
+
+// evaluator.cpp:216-239
+PuctNode* PuctEvaluator::expandChild(PuctNode* parent, PuctNodeChild* child) {
+    sm->updateBases(parent->getBaseState());
+    sm->nextState(child->move, basestate_expand_node.data());
+
+    const int next_depth = parent->game_depth + 1;
+    child->to_node = lookupNode(basestate_expand_node.data(), next_depth);
+    if (child->to_node != nullptr) {
+        child->to_node->ref_count++;
+        stats.num_transpositions_attached++;
+    } else {
+        child->unselectable = true;
+        parent->unselectable_count++;
+        child->to_node = createNode(parent, basestate_expand_node.data());
+        parent->unselectable_count--;
+        child->unselectable = false;
+    }
+    return child->to_node;
+}
+
+typedef std::vector<PuctNodeChild*> SortedChildren;
+
+// evaluator.cpp:242-263: by current score of the lead role desc; unexpanded (-1) by prior desc
+static SortedChildren sortedChildrenSelect(PuctNode* node) {
+    SortedChildren children;
+    children.reserve(node->num_children);
+    for (int ii = 0; ii < node->num_children; ii++) children.push_back(node->getNodeChild(0, ii));
+    auto f = [node](const PuctNodeChild* a, const PuctNodeChild* b) {
+        const float sa = a->to_node == nullptr ? -1 : a->to_node->getCurrentScore(node->lead_role_index);
+        const float sb = b->to_node == nullptr ? -1 : b->to_node->getCurrentScore(node->lead_role_index);
+        if (sa < 0 && sb < 0) return a->policy_prob_orig > b->policy_prob_orig;
+        return sa > sb;
+    };
+    std::sort(children.begin(), children.end(), f);
+    return children;
+}
+
+// evaluator.cpp:266-279
+static SortedChildren sortedTraversals(PuctNode* node) {
+    SortedChildren children;
+    for (int ii = 0; ii < node->num_children; ii++) children.push_back(node->getNodeChild(0, ii));
+    auto f = [](const PuctNodeChild* a, const PuctNodeChild* b) { return a->traversals > b->traversals; };
+    std::sort(children.begin(), children.end(), f);
+    return children;
+}
+
+// evaluator.cpp:282-339
+void PuctEvaluator::balanceFirstMoves(int max_moves) {
+    GZ_ASSERT(root != nullptr);
+    if (root->isTerminal()) return;
+    max_moves = std::min(max_moves, (int)root->num_children);
+    auto children = sortedTraversals(root);
+    int wanted_traversals = -1;
+    for (int ii = 0; ii < max_moves; ii++) {
+        PuctNodeChild* child = children[ii];
+        if (ii == 0) {
+            wanted_traversals = child->traversals;
+            continue;
+        }
+        while ((int)child->traversals < wanted_traversals) {
+            PuctNode* temp_root = child->to_node;
+            if (temp_root == nullptr || temp_root->isTerminal()) break;
+            int worker_count = 0;
+            auto f = [this, child, temp_root, &worker_count]() {
+                Path path;
+                path.emplace_back(this->root, child, child);
+                this->treePlayout(temp_root, path);
+                worker_count--;
+            };
+            for (int jj = 0; jj < conf->batch_size; jj++) {
+                worker_count++;
+                scheduler->addRunnable(f);
+            }
+            while (worker_count > 0) scheduler->yield();
+        }
+    }
+}
+
+// evaluator.cpp:341-517
+PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
+    GZ_ASSERT(!node->isTerminal());
+    const int depth = (int)path.size();
+    setPuctConstant(node, depth);
+
+    if (node->num_children == 1) {
+        PuctNodeChild* child = node->getNodeChild(0, 0);
+        path.emplace_back(node, child, child);
+        return child;
+    }
+
+    if (depth == 0) setDirichletNoise(node);
+
+    const float prior_score = priorScore(node, depth);
+    const double sqrt_node_visits = std::sqrt(node->visits + 1);
+
+    float best_score = -1;
+    PuctNodeChild* best_child = nullptr;
+    float best_child_score_actual_score = -1;
+    PuctNodeChild* best_child_score = nullptr;
+    PuctNodeChild* bad_fallback = nullptr;
+    float best_fallback_score = -1;
+    PuctNodeChild* best_fallback = nullptr;
+    int unselectables = 0;
+
+    SortedChildren children = sortedChildrenSelect(node);
+    for (PuctNodeChild* c : children) {
+        if (c->unselectable) {
+            unselectables++;
+            continue;
+        } else if (c->to_node != nullptr && (c->to_node->num_children > 0 &&
+                                             c->to_node->unselectable_count == c->to_node->num_children)) {
+            unselectables++;
+            continue;
+        }
+
+        double child_score = prior_score;
+        const int traversals = c->traversals + 1;
+        const double inflight_visits = c->to_node != nullptr ? c->to_node->inflight_visits : 0;
+        double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
+                                   (traversals + inflight_visits);
+
+        if (c->to_node != nullptr) {
+            PuctNode* cn = c->to_node;
+            child_score = cn->getCurrentScore(node->lead_role_index);
+            if (cn->is_finalised) {
+                if (child_score > 0.99) {
+                    if (depth > 0) {
+                        path.emplace_back(node, c, c);
+                        return c;
+                    }
+                    child_score *= 1.0f + node->puct_constant;
+                } else if (child_score < 0.01) {
+                    bad_fallback = c;
+                    continue;
+                } else {
+                    exploration_score = 0.0;
+                }
+            }
+            if ((cn->is_finalised || cn->visits > 42) && child_score > best_child_score_actual_score) {
+                best_child_score_actual_score = child_score;
+                best_child_score = c;
+            }
+        }
+
+        if (c->traversals > 0 && inflight_visits > 0) {
+            const double discounted_visits = inflight_visits * (rng.get() + 0.5);
+            child_score = (child_score * c->traversals) / (c->traversals + discounted_visits);
+        }
+
+        const float limit_latch_root = 0.66;
+        c->debug_node_score = child_score;
+        c->debug_puct_score = exploration_score;
+        const double score = child_score + exploration_score;
+
+        if (node->visits > 1000 && node->visits < 40000000 && depth == 0 && rng.get() > 0.1) {
+            if (c->traversals > 16 && c->traversals > node->visits * limit_latch_root) {
+                if (best_fallback == nullptr || score > best_fallback_score) {
+                    best_fallback = c;
+                    best_fallback_score = score;
+                }
+                continue;
+            }
+        }
+
+        if (score > best_score) {
+            best_child = c;
+            best_score = score;
+        }
+    }
+
+    if (best_child == nullptr) {
+        if (best_fallback != nullptr) {
+            best_child = best_child_score != nullptr ? best_child_score : best_fallback;
+        } else if (bad_fallback != nullptr) {
+            if (unselectables > 0) scheduler->yield();
+            best_child = bad_fallback;
+        } else {
+            stats.num_blocked++;
+        }
+    }
+    if (best_child_score == nullptr) best_child_score = best_child;
+    if (best_child != nullptr) path.emplace_back(node, best_child, best_child_score);
+    return best_child;
+}
+
+// evaluator.cpp:519-656
+void PuctEvaluator::backup(float* new_scores, const Path& path) {
+    const int role_count = sm->roleCount();
+    auto forceFinalise = [role_count](PuctNode* cur) -> const PuctNodeChild* {
+        float best_score = -1;
+        const PuctNodeChild* best = nullptr;
+        bool more_to_explore = false;
+        for (int ii = 0; ii < cur->num_children; ii++) {
+            const PuctNodeChild* c = cur->getNodeChild(role_count, ii);
+            if (c->to_node != nullptr && c->to_node->is_finalised) {
+                const float score = c->to_node->getCurrentScore(cur->lead_role_index);
+                if (score > 0.99) return c;
+                if (score > best_score) {
+                    best_score = score;
+                    best = c;
+                }
+            } else {
+                more_to_explore = true;
+            }
+        }
+        return more_to_explore ? nullptr : best;
+    };
+
+    bool bp_finalised_only_once = conf->backup_finalised;
+    for (int index = (int)path.size() - 1; index >= 0; index--) {
+        const PathElement& cur = path[index];
+        if (bp_finalised_only_once && !cur.node->is_finalised && cur.node->lead_role_index >= 0) {
+            bp_finalised_only_once = false;
+            const PuctNodeChild* finalised_child = forceFinalise(cur.node);
+            if (finalised_child != nullptr) {
+                for (int ii = 0; ii < role_count; ii++)
+                    cur.node->setCurrentScore(ii, finalised_child->to_node->getCurrentScore(ii));
+                cur.node->is_finalised = true;
+            }
+        }
+
+        if (cur.node->is_finalised) {
+            for (int ii = 0; ii < role_count; ii++) new_scores[ii] = cur.node->getCurrentScore(ii);
+        } else {
+            for (int ii = 0; ii < role_count; ii++) {
+                float visits = cur.node->visits;
+                if (visits > 100000) visits = 100000 + 0.1f * (visits - 100000);
+                const float score = ((visits * cur.node->getCurrentScore(ii) + new_scores[ii]) / (visits + 1.0f));
+                cur.node->setCurrentScore(ii, score);
+            }
+        }
+
+        cur.node->visits++;
+        if (cur.node->inflight_visits > 0) cur.node->inflight_visits--;
+
+        if (cur.choice != nullptr) {
+            cur.choice->traversals++;
+            if (cur.node->visits > 23) {
+                const float cur_score = cur.node->getCurrentScore(cur.node->lead_role_index);
+                float apply, minimum;
+                if (cur_score > 0.3 && cur_score < 0.7) {
+                    apply = 0.995;
+                    minimum = 0.02f;
+                } else if (cur_score > 0.15 && cur_score < 0.85) {
+                    apply = 0.9975;
+                    minimum = 0.03f;
+                } else {
+                    apply = 0.9975;
+                    minimum = 0.10f;
+                }
+                if (cur.choice->policy_prob > minimum) {
+                    cur.choice->policy_prob *= apply;
+                    cur.choice->policy_prob = std::max(minimum, cur.choice->policy_prob);
+                }
+            }
+        }
+
+        if (cur.node->visits % 100 == 0) cur.node->normaliseX();
+    }
+}
+
+// evaluator.cpp:658-720
+int PuctEvaluator::treePlayout(PuctNode* current, Path& path) {
+    GZ_ASSERT(current != nullptr && !current->isTerminal());
+    float scores[kMaxRoles];
+    PuctNodeChild* child = nullptr;
+
+    while (true) {
+        if (current->isTerminal()) {
+            path.emplace_back(current, nullptr, nullptr);
+            break;
+        }
+        if (current->is_finalised) {
+            path.emplace_back(current, nullptr, nullptr);
+            break;
+        }
+        while (true) {
+            child = selectChild(current, path);
+            if (child != nullptr) break;
+            scheduler->yield();
+        }
+        if (child->to_node == nullptr) {
+            current = expandChild(current, child);
+            if (current->is_finalised || current->num_children > 1) {
+                path.emplace_back(current, nullptr, nullptr);
+                break;
+            }
+        }
+        current->inflight_visits++;
+        current = child->to_node;
+    }
+
+    if (current->is_finalised) stats.playouts_finals++;
+    for (int ii = 0; ii < sm->roleCount(); ii++) scores[ii] = current->getCurrentScore(ii);
+    backup(scores, path);
+    stats.num_tree_playouts++;
+    return (int)path.size();
+}
+
+// evaluator.cpp:722-742
+void PuctEvaluator::playoutWorker(int) {
+    while (do_playouts) {
+        if (stats.num_tree_playouts % 10000 == 0) scheduler->yield();
+        if (root->is_finalised) break;
+        Path path;
+        const int depth = treePlayout(root, path);
+        stats.playouts_max_depth = std::max(depth, stats.playouts_max_depth);
+        stats.playouts_total_depth += depth;
+    }
+}
+
+// evaluator.cpp:744-886 (verbose reporting omitted)
+void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
+    const double start_time = get_time();
+    const bool use_think_time = conf->think_time > 0;
+    auto elapsed = [start_time](double t) { return get_time() > (start_time + t); };
+
+    const int max_non_converged_evaluations = max_evaluations * conf->evaluation_multiplier_to_convergence;
+    const int max_tree_playouts = 4 * max_non_converged_evaluations;
+
+    Path path;
+    while (true) {
+        const int our_role_index = root->lead_role_index;
+        const bool is_converged = converged(conf->converged_visits);
+
+        if (end_time > 0 && get_time() > end_time) break;
+        if (root->is_finalised && stats.num_tree_playouts > 100) break;
+        if (is_converged && stats.num_tree_playouts > max_tree_playouts) break;
+        if (number_of_nodes > 50000000) break;
+        if (is_converged && stats.num_evaluations > max_evaluations) break;
+        if (!is_converged && stats.num_evaluations > max_non_converged_evaluations) break;
+        if (use_think_time) {
+            if (is_converged && elapsed(conf->think_time)) break;
+            if (!is_converged && elapsed(conf->think_time * conf->evaluation_multiplier_to_convergence)) break;
+            if (elapsed(120.0) && is_converged) {
+                const PuctNodeChild* best = chooseTopVisits(root);
+                if (best->to_node->getCurrentScore(our_role_index) > 0.975 ||
+                    best->to_node->getCurrentScore(our_role_index) < 0.025)
+                    break;
+            }
+        }
+
+        path.clear();
+        const int depth = treePlayout(root, path);
+        stats.playouts_max_depth = std::max(depth, stats.playouts_max_depth);
+        stats.playouts_total_depth += depth;
+    }
+}
+
+// evaluator.cpp:888-943
+PuctNode* PuctEvaluator::fastApplyMove(const PuctNodeChild* next) {
+    GZ_ASSERT(root != nullptr && initial_root != nullptr);
+    PuctNode* new_root = nullptr;
+    for (int ii = 0; ii < root->num_children; ii++) {
+        PuctNodeChild* c = root->getNodeChild(0, ii);
+        if (c == next) {
+            GZ_ASSERT(new_root == nullptr);
+            if (c->to_node == nullptr) expandChild(root, c);
+            new_root = c->to_node;
+        } else if (c->to_node != nullptr) {
+            PuctNode* next_node = c->to_node;
+            c->to_node = nullptr;
+            GZ_ASSERT(next_node->ref_count > 0);
+            next_node->ref_count--;
+            if (next_node->ref_count == 0) {
+                releaseNodes(next_node);
+                garbage.push_back(next_node);
+            }
+        }
+    }
+    for (PuctNode* n : garbage) removeNode(n);
+    garbage.clear();
+
+    GZ_ASSERT(new_root != nullptr);
+    root = new_root;
+    game_depth++;
+    return root;
+}
+
+// evaluator.cpp:945-969
+void PuctEvaluator::applyMove(const JointMove* move) {
+    for (int ii = 0; ii < root->num_children; ii++) {
+        PuctNodeChild* c = root->getNodeChild(0, ii);
+        if (c->move.equals(*move, sm->roleCount())) {
+            fastApplyMove(c);
+            break;
+        }
+    }
+    GZ_ASSERT(root != nullptr);
+}
+
+// evaluator.cpp:971-1004
+void PuctEvaluator::reset(int depth) {
+    if (initial_root != nullptr) {
+        releaseNodes(initial_root);
+        garbage.push_back(initial_root);
+        for (PuctNode* n : garbage) removeNode(n);
+        garbage.clear();
+        initial_root = root = nullptr;
+    }
+    stats.reset();
+    game_depth = depth;
+}
+
+// evaluator.cpp:1006-1017
+PuctNode* PuctEvaluator::establishRoot(const uint64_t* current_state) {
+    GZ_ASSERT(root == nullptr && initial_root == nullptr);
+    if (current_state == nullptr) current_state = sm->initialState();
+    initial_root = root = createNode(nullptr, current_state);
+    GZ_ASSERT(!root->isTerminal());
+    return root;
+}
+
+// evaluator.cpp:1019-1030
+void PuctEvaluator::resetRootNode() {
+    GZ_ASSERT(root != nullptr);
+    for (int ii = 0; ii < root->num_children; ii++) {
+        PuctNodeChild* c = root->getNodeChild(0, ii);
+        c->policy_prob = c->policy_prob_orig;
+        c->traversals = std::min(1U, c->traversals);
+    }
+    root->dirichlet_noise_set = false;
+}
+
+// evaluator.cpp:1032-1098
+const PuctNodeChild* PuctEvaluator::onNextMove(int max_evaluations, double end_time) {
+    GZ_ASSERT(root != nullptr && initial_root != nullptr);
+    stats.reset();
+    do_playouts = true;
+
+    if (conf->think_time > 10 && !root->dirichlet_noise_set && !root->is_finalised && root->visits > 10000) {
+        if (number_of_nodes < 3000000) resetRootNode();
+    }
+
+    int worker_count = 0;
+    auto f = [this, &worker_count]() {
+        this->playoutWorker(worker_count);
+        worker_count--;
+    };
+    if (conf->batch_size > 1 && root != nullptr && !root->is_finalised) {
+        if (max_evaluations < 0 || max_evaluations > 100) {
+            for (int ii = 0; ii < conf->batch_size - 1; ii++) {
+                worker_count++;
+                scheduler->addRunnable(f);
+            }
+        }
+    }
+
+    if (max_evaluations != 0) playoutMain(max_evaluations, end_time);
+
+    do_playouts = false;
+    while (worker_count > 0) scheduler->yield();
+
+    return choose(root);
+}
+
+// evaluator.cpp:1100-1159
+const PuctNodeChild* PuctEvaluator::chooseTopVisits(const PuctNode* node) const {
+    GZ_ASSERT(node != nullptr);
+    Children children = PuctNode::sortedChildrenTraversals(node);
+    GZ_ASSERT(!children.empty());
+    const int role_index = node->lead_role_index;
+    int indx0 = -1, indx1 = -1;
+    int count = 0;
+    for (const PuctNodeChild* c : children) {
+        if (c->to_node != nullptr && c->to_node->is_finalised) {
+            if (c->to_node->getCurrentScore(role_index) > 0.99) return c;
+            if (c->to_node->getCurrentScore(role_index) < 0.01) {
+                count++;
+                continue;
+            }
+        }
+        if (indx0 == -1) indx0 = count;
+        else if (indx1 == -1) indx1 = count;
+        count++;
+    }
+    if (conf->top_visits_best_guess_converge_ratio > 0 && indx0 != -1 && indx1 != -1) {
+        const PuctNodeChild* c0 = children[indx0];
+        const PuctNodeChild* c1 = children[indx1];
+        if (c0->to_node != nullptr && c1->to_node != nullptr) {
+            if (c1->traversals > c0->traversals * conf->top_visits_best_guess_converge_ratio &&
+                c1->to_node->getCurrentScore(role_index) > c0->to_node->getCurrentScore(role_index))
+                return c1;
+            return c0;
+        }
+    }
+    return children[0];
+}
+
+// evaluator.cpp:1161-1192.  next_prob = pow(next_prob, temperature): the reference writes
+// ::pow(float, float); this build evaluates it as the C library's double pow() and stores a float.
+Children PuctEvaluator::getProbabilities(PuctNode* node, float temperature, bool use_policy) {
+    GZ_ASSERT(node->num_children > 0);
+    const float node_visits = node->visits + 0.001 * node->num_children;
+    float total_probability = 0.0f;
+    for (int ii = 0; ii < node->num_children; ii++) {
+        PuctNodeChild* child = node->getNodeChild(0, ii);
+        const float child_visits = child->to_node ? child->traversals + 0.001f : 0.001f;
+        if (use_policy) child->next_prob = child->policy_prob + 0.001f;
+        else child->next_prob = child_visits / node_visits;
+        child->next_prob = (float)::pow((double)child->next_prob, (double)temperature);
+        total_probability += child->next_prob;
+    }
+    for (int ii = 0; ii < node->num_children; ii++) node->getNodeChild(0, ii)->next_prob /= total_probability;
+    return PuctNode::sortedChildren(node, true);
+}
+
+// evaluator.cpp:1195-1224
+float PuctEvaluator::priorScore(PuctNode* node, int depth) const {
+    float prior_score = node->getFinalScore(node->lead_role_index);
+    if (node->visits > 8) {
+        const PuctNodeChild* best = chooseTopVisits(node);
+        if (best->to_node != nullptr) prior_score = best->to_node->getCurrentScore(node->lead_role_index);
+    }
+    float fpu_reduction = depth == 0 ? conf->fpu_prior_discount_root : conf->fpu_prior_discount;
+    if (fpu_reduction > 0) {
+        float total_policy_visited = 0.0;
+        for (int ii = 0; ii < node->num_children; ii++) {
+            const PuctNodeChild* c = node->getNodeChild(0, ii);
+            if (c->to_node != nullptr && c->to_node->visits > 0) total_policy_visited += c->policy_prob;
+        }
+        fpu_reduction *= std::sqrt(total_policy_visited);
+        prior_score -= fpu_reduction;
+    }
+    return prior_score;
+}
+
+// evaluator.cpp:1227-1297
+void PuctEvaluator::setDirichletNoise(PuctNode* node) {
+    if (node->dirichlet_noise_set || node->num_children < 2 || conf->dirichlet_noise_pct < 0) return;
+    if (node->getCurrentScore(node->lead_role_index) > 0.95) return;
+
+    const float dirichlet_noise_alpha = 10.83f / node->num_children;
+    std::gamma_distribution<float> gamma(dirichlet_noise_alpha, 1.0f);
+    std::vector<float> dirichlet_noise(node->num_children, 0.0f);
+    float total_noise = 0.0f;
+    for (int ii = 0; ii < node->num_children; ii++) {
+        const float noise = gamma(rng);
+        dirichlet_noise[ii] = noise;
+        total_noise += noise;
+    }
+    if (total_noise < std::numeric_limits<float>::min()) return;
+    for (int ii = 0; ii < node->num_children; ii++) dirichlet_noise[ii] /= total_noise;
+
+    const bool policy_squash = (conf->noise_policy_squash_pct > 0 && rng.get() < conf->noise_policy_squash_pct);
+    float total_policy = 0;
+    for (int ii = 0; ii < node->num_children; ii++) {
+        PuctNodeChild* c = node->getNodeChild(0, ii);
+        if (policy_squash) c->policy_prob = std::min(conf->noise_policy_squash_prob, c->policy_prob);
+        const float pct = conf->dirichlet_noise_pct;
+        c->policy_prob = (1.0f - pct) * c->policy_prob + pct * dirichlet_noise[ii];
+        total_policy += c->policy_prob;
+    }
+    for (int ii = 0; ii < node->num_children; ii++) node->getNodeChild(0, ii)->policy_prob /= total_policy;
+    node->dirichlet_noise_set = true;
+}
+
+// evaluator.cpp:1300-1307
+void PuctEvaluator::setPuctConstant(PuctNode* node, int depth) const {
+    const float cpuct_base_id = 19652.0f;
+    const float puct_constant = depth == 0 ? conf->puct_constant_root : conf->puct_constant;
+    node->puct_constant = std::log((1 + node->visits + cpuct_base_id) / cpuct_base_id);
+    node->puct_constant += puct_constant;
+}
+
+// evaluator.cpp:1309-1322
+float PuctEvaluator::getTemperature(int depth) const {
+    if (depth >= conf->depth_temperature_stop) return -1;
+    float multiplier = 1.0f + ((depth - conf->depth_temperature_start) * conf->depth_temperature_increment);
+    multiplier = std::max(1.0f, multiplier);
+    return std::min(conf->temperature * multiplier, conf->depth_temperature_max);
+}
+
+// evaluator.cpp:1324-1340
+const PuctNodeChild* PuctEvaluator::choose(const PuctNode* node) {
+    if (conf->choose == ChooseFn::choose_temperature) return chooseTemperature(node);
+    return chooseTopVisits(node);
+}
+
+// evaluator.cpp:1342-1362
+bool PuctEvaluator::converged(int count) const {
+    Children children = PuctNode::sortedChildren(root);
+    if (children.size() >= 2) {
+        PuctNode* n0 = children[0]->to_node;
+        PuctNode* n1 = children[1]->to_node;
+        if (n0 != nullptr && n1 != nullptr) {
+            const int role_index = root->lead_role_index;
+            if (n0->getCurrentScore(role_index) > n1->getCurrentScore(role_index) && n0->visits > n1->visits + count)
+                return true;
+        }
+        return false;
+    }
+    return true;
+}
+
+// evaluator.cpp:1473-1510
+const PuctNodeChild* PuctEvaluator::chooseTemperature(const PuctNode* node) {
+    if (node == nullptr) node = root;
+    const float temperature = getTemperature(node->game_depth);
+    if (temperature < 0) return chooseTopVisits(node);
+    Children dist;
+    if (conf->dirichlet_noise_pct < 0 && node->visits < 3) dist = getProbabilities(root, temperature, true);
+    else dist = getProbabilities(root, temperature, false);
+    const float expected_probability = rng.get() * conf->random_scale;
+    float seen_probability = 0;
+    for (const PuctNodeChild* c : dist) {
+        seen_probability += c->next_prob;
+        if (seen_probability > expected_probability) return c;
+    }
+    return dist.back();
+}
+
+// node.cpp:400-441 (PuctNode::debug), sorted by traversals then lead-role score
+void PuctEvaluator::nodeDebug(int child_index, int max_variation_depth, PuctNodeDebug& info) const {
+    const PuctNode* node = root;
+    if (node == nullptr || child_index >= node->num_children) return;
+    Children node_children;
+    for (int ii = 0; ii < node->num_children; ii++) node_children.push_back(node->getNodeChild(0, ii));
+    const int ri = node->lead_role_index;
+    std::sort(node_children.begin(), node_children.end(), [ri](const PuctNodeChild* a, const PuctNodeChild* b) {
+        if (a->traversals != b->traversals) return a->traversals > b->traversals;
+        const float a_prob = a->to_node != nullptr ? a->to_node->getCurrentScore(ri) : -1.0f;
+        const float b_prob = b->to_node != nullptr ? b->to_node->getCurrentScore(ri) : -1.0f;
+        return a_prob > b_prob;
+    });
+    const PuctNodeChild* child = node_children[child_index];
+    if (child->to_node == nullptr) return;
+    info.lead_role_index = node->lead_role_index;
+    info.score = child->to_node->getCurrentScore(node->lead_role_index);
+    info.move_index = child->move.get(node->lead_role_index);
+    const PuctNode* cur = child->to_node;
+    for (int ii = 0; ii < max_variation_depth; ii++) {
+        if (cur == nullptr || cur->num_children == 0 || cur->visits < 100) return;
+        Children cc = PuctNode::sortedChildrenTraversals(cur, false);
+        const PuctNodeChild* top = cc[0];
+        info.variation.emplace_back(cur->lead_role_index, top->move.get(cur->lead_role_index));
+        cur = top->to_node;
+    }
+}
+
+}  // namespace gz

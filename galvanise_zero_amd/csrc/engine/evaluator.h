@@ -1,0 +1,126 @@
+// PUCT evaluator: restates PuctEvaluator (reference src/cpp/puct/evaluator.h:31-160,
+// evaluator.cpp:37-1510).  One instance per game; it owns the game tree and asks its scheduler for
+// a network evaluation of every new non-trivial node (the coroutine parks inside evaluate()).
+#pragma once
+
+#include "config.h"
+#include "node.h"
+#include "rng.h"
+#include "scheduler.h"
+
+#include <unordered_map>
+#include <vector>
+
+namespace gz {
+
+struct PathElement {
+    PathElement(PuctNode* node, PuctNodeChild* choice, PuctNodeChild* best)
+        : node(node), choice(choice), best(best) {}
+    PuctNode* node;
+    PuctNodeChild* choice;
+    PuctNodeChild* best;
+};
+using Path = std::vector<PathElement>;
+
+struct PuctNodeDebug {
+    float score = 0;
+    int lead_role_index = 0;
+    int move_index = 0;
+    std::vector<std::pair<int, int>> variation;
+};
+
+class PuctEvaluator {
+public:
+    PuctEvaluator(StateMachine* sm, NetworkScheduler* scheduler, const GdlBasesTransformer* transformer);
+    ~PuctEvaluator();
+
+    void updateConf(const PuctConfig* conf);
+    void seed(uint64_t s) { rng.seed(s); }
+
+    void setDirichletNoise(PuctNode* node);
+    float priorScore(PuctNode* node, int depth) const;
+    void setPuctConstant(PuctNode* node, int depth) const;
+    float getTemperature(int depth) const;
+
+    const PuctNodeChild* choose(const PuctNode* node);
+    bool converged(int count) const;
+
+    PuctNode* expandChild(PuctNode* parent, PuctNodeChild* child);
+    void balanceFirstMoves(int max_moves);
+
+    void reset(int game_depth);
+    PuctNode* fastApplyMove(const PuctNodeChild* next);
+    PuctNode* establishRoot(const uint64_t* current_state);
+    void resetRootNode();
+    const PuctNodeChild* onNextMove(int max_evaluations, double end_time = -1);
+    void applyMove(const JointMove* move);
+
+    const PuctNodeChild* chooseTopVisits(const PuctNode* node) const;
+    const PuctNodeChild* chooseTemperature(const PuctNode* node);
+    Children getProbabilities(PuctNode* node, float temperature, bool use_policy = true);
+
+    int nodeCount() const { return number_of_nodes; }
+    StateMachine* getSM() const { return sm; }
+    const PuctNode* getRootNode() const { return root; }
+    PuctNode* getRootNodeMutable() { return root; }
+
+    void nodeDebug(int child_index, int max_variation_depth, PuctNodeDebug& info) const;
+
+    // per onNextMove statistics (evaluator.h:101-125)
+    struct PlayoutStats {
+        void reset() { *this = PlayoutStats(); }
+        int num_blocked = 0;
+        int num_tree_playouts = 0;
+        int num_evaluations = 0;
+        int num_transpositions_attached = 0;
+        int playouts_total_depth = 0;
+        int playouts_max_depth = 0;
+        int playouts_finals = 0;
+    };
+    const PlayoutStats& getStats() const { return stats; }
+    long totalEvaluations() const { return total_evaluations; }
+
+private:
+    void removeNode(PuctNode*);
+    void releaseNodes(PuctNode*);
+    PuctNode* lookupNode(const uint64_t* bs, int depth);
+    PuctNode* createNode(PuctNode* parent, const uint64_t* state);
+    PuctNodeChild* selectChild(PuctNode* node, Path& path);
+    void backup(float* new_scores, const Path& path);
+    int treePlayout(PuctNode* current, Path& path);
+    void playoutWorker(int worker_id);
+    void playoutMain(int max_evaluations, double end_time);
+
+    struct MaskedKey {
+        std::vector<uint64_t> w;
+        bool operator==(const MaskedKey& o) const { return w == o.w; }
+    };
+    struct MaskedHash {
+        size_t operator()(const MaskedKey& k) const;
+    };
+    MaskedKey maskedKey(const uint64_t* bs) const;
+
+    const PuctConfig* conf = nullptr;
+    StateMachine* sm;
+    std::vector<uint64_t> basestate_expand_node;
+    NetworkScheduler* scheduler;
+    std::vector<uint64_t> hash_mask;
+
+    int game_depth = 0;
+    PuctNode* initial_root = nullptr;
+    PuctNode* root = nullptr;
+
+    std::unordered_map<MaskedKey, PuctNode*, MaskedHash> lookup;
+    std::vector<PuctNode*> garbage;
+
+    int number_of_nodes = 0;
+    long node_allocated_memory = 0;
+    long total_evaluations = 0;
+    bool do_playouts = false;
+    PlayoutStats stats;
+    Rng rng;
+};
+
+double get_time();
+
+}  // namespace gz

@@ -1,0 +1,209 @@
+#include "node.h"
+
+#include "transformer.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <limits>
+
+namespace gz {
+
+static size_t node_bytes(int num_children, int role_count, int num_words) {
+    size_t n = sizeof(PuctNode) + sizeof(PuctNodeChild) * num_children + sizeof(Score) * 2 * role_count;
+    n = (n + 7) & ~size_t(7);
+    return n + sizeof(uint64_t) * num_words;
+}
+
+// node.cpp:111-149: children = cross product of every role's legal moves, role 0 outermost.
+static int initialiseChildHelper(PuctNode* node, int role_index, int child_index, int role_count,
+                                 StateMachine* sm, JointMove* joint_move) {
+    const bool final_role = role_index == role_count - 1;
+    const int n = sm->legalCount(role_index);
+    for (int ii = 0; ii < n; ++ii) {
+        joint_move->set(role_index, sm->legal(role_index, ii));
+        if (final_role) {
+            PuctNodeChild* child = node->getNodeChild(role_count, child_index++);
+            child->to_node = nullptr;
+            child->unselectable = false;
+            child->use_minimax = false;
+            child->traversals = 0;
+            child->policy_prob_orig = 1.0f;
+            child->policy_prob = 1.0f;
+            child->next_prob = 0.0f;
+            child->debug_node_score = 0.0f;
+            child->debug_puct_score = 0.0f;
+            child->move = *joint_move;
+        } else {
+            child_index = initialiseChildHelper(node, role_index + 1, child_index, role_count, sm, joint_move);
+        }
+    }
+    return child_index;
+}
+
+// node.cpp:42-109 + 153-221
+PuctNode* PuctNode::create(const uint64_t* base_state, StateMachine* sm) {
+    const int role_count = sm->roleCount();
+    const int num_words = sm->numWords();
+    sm->updateBases(base_state);
+
+    int lead_role_index = 0;
+    bool is_finalised = true;
+    int total_children = 0;
+    if (!sm->isTerminal()) {
+        total_children = 1;
+        is_finalised = false;
+        int max_moves_for_a_role = 1;
+        for (int ri = 0; ri < role_count; ++ri) {
+            const int c = sm->legalCount(ri);
+            total_children *= c;
+            if (c > max_moves_for_a_role) {
+                max_moves_for_a_role = c;
+                lead_role_index = ri;
+            }
+        }
+        if (max_moves_for_a_role > 1) {
+            bool rest_one = true;
+            for (int ri = 0; ri < role_count; ++ri)
+                if (ri != lead_role_index && sm->legalCount(ri) > 1) rest_one = false;
+            if (!rest_one) lead_role_index = PuctNode::lead_role_index_simultaneous;
+        }
+    }
+
+    const size_t bytes = node_bytes(total_children, role_count, num_words);
+    PuctNode* node = static_cast<PuctNode*>(std::malloc(bytes));
+    node->parent = nullptr;
+    node->visits = 0;
+    node->inflight_visits = 0;
+    node->ref_count = 1;
+    node->unselectable_count = 0;
+    node->num_children = (uint16_t)total_children;
+    node->num_children_expanded = 0;
+    node->puct_constant = 1.44f;
+    node->is_finalised = is_finalised;
+    node->force_terminal = false;
+    node->dirichlet_noise_set = false;
+    node->lead_role_index = (int16_t)lead_role_index;
+    node->game_depth = 0;
+    node->role_count = (uint8_t)role_count;
+    node->num_words = (uint16_t)num_words;
+    node->allocated_size = (uint32_t)bytes;
+    for (int ii = 0; ii < role_count; ++ii) {
+        node->setFinalScore(ii, 0.0f);
+        node->setCurrentScore(ii, 0.0f);
+    }
+    std::copy(base_state, base_state + num_words, node->getBaseState());
+
+    if (!node->is_finalised) {
+        JointMove move{};
+        const int count = initialiseChildHelper(node, 0, 0, role_count, sm, &move);
+        (void)count;
+    } else {
+        for (int ii = 0; ii < role_count; ++ii) {
+            const int score = sm->goalValue(ii);
+            node->setFinalScore(ii, score / 100.0);
+            node->setCurrentScore(ii, score / 100.0);
+        }
+    }
+    return node;
+}
+
+void PuctNode::destroy(PuctNode* n) { std::free(n); }
+
+void PuctNode::normaliseX() {
+    float total_prediction = 0;
+    for (int ii = 0; ii < num_children; ii++) total_prediction += children()[ii].policy_prob;
+    if (total_prediction > std::numeric_limits<float>::min()) {
+        for (int ii = 0; ii < num_children; ii++) children()[ii].policy_prob /= total_prediction;
+    } else {
+        for (int ii = 0; ii < num_children; ii++) children()[ii].policy_prob = 1.0 / num_children;
+    }
+}
+
+// node.cpp:316-343: by to_node visits desc, ties by next_prob / policy_prob desc (std::sort)
+Children PuctNode::sortedChildren(const PuctNode* node, bool next_probability) {
+    Children children;
+    children.reserve(node->num_children);
+    for (int ii = 0; ii < node->num_children; ii++) children.push_back(node->getNodeChild(0, ii));
+    auto f = [next_probability](const PuctNodeChild* a, const PuctNodeChild* b) {
+        const int visits_a = a->to_node == nullptr ? 0 : a->to_node->visits;
+        const int visits_b = b->to_node == nullptr ? 0 : b->to_node->visits;
+        if (visits_a == visits_b) {
+            if (next_probability) return a->next_prob > b->next_prob;
+            return a->policy_prob > b->policy_prob;
+        }
+        return visits_a > visits_b;
+    };
+    std::sort(children.begin(), children.end(), f);
+    return children;
+}
+
+// node.cpp:346-373: by traversals desc, ties by next_prob / policy_prob desc (std::sort)
+Children PuctNode::sortedChildrenTraversals(const PuctNode* node, bool next_probability) {
+    Children children;
+    children.reserve(node->num_children);
+    for (int ii = 0; ii < node->num_children; ii++) children.push_back(node->getNodeChild(0, ii));
+    auto f = [next_probability](const PuctNodeChild* a, const PuctNodeChild* b) {
+        const int traversals_a = a->traversals;
+        const int traversals_b = b->traversals;
+        if (traversals_a == traversals_b) {
+            if (next_probability) return a->next_prob > b->next_prob;
+            return a->policy_prob > b->policy_prob;
+        }
+        return traversals_a > traversals_b;
+    };
+    std::sort(children.begin(), children.end(), f);
+    return children;
+}
+
+std::string PuctNode::moveString(const JointMove& move, const StateMachine* sm) {
+    std::string res = "(";
+    for (int ii = 0; ii < sm->roleCount(); ii++) {
+        if (ii > 0) res += " ";
+        res += sm->legalToMove(ii, move.get(ii));
+    }
+    return res + ")";
+}
+
+// node.cpp:449-461: planes of this node + its parent chain (num_prev_states of them)
+void PuctNodeRequest::add(float* buf, const GdlBasesTransformer* transformer) const {
+    std::vector<const uint64_t*> prev_states;
+    const PuctNode* cur = node->parent;
+    for (int ii = 0; ii < transformer->getNumberPrevStates(); ii++) {
+        if (cur != nullptr) {
+            prev_states.push_back(cur->getBaseState());
+            cur = cur->parent;
+        }
+    }
+    transformer->toChannels(node->getBaseState(), prev_states, buf);
+}
+
+// node.cpp:463-511
+void PuctNodeRequest::reply(const ModelResult& result, const GdlBasesTransformer* transformer) {
+    const int role_count = transformer->getNumberPolicies();
+    float total_prediction = 0.0f;
+    const float* raw_policy = result.getPolicy(node->lead_role_index);
+    for (int ii = 0; ii < node->num_children; ii++) {
+        PuctNodeChild* c = node->getNodeChild(role_count, ii);
+        c->policy_prob_orig = raw_policy[c->move.get(node->lead_role_index)];
+        c->policy_prob_orig = std::max(0.001f, c->policy_prob_orig);
+        total_prediction += c->policy_prob_orig;
+    }
+    for (int ii = 0; ii < node->num_children; ii++) {
+        PuctNodeChild* c = node->getNodeChild(role_count, ii);
+        c->policy_prob_orig /= total_prediction;
+        c->policy_prob = c->policy_prob_orig;
+    }
+    for (int ri = 0; ri < role_count; ri++) {
+        float s = result.getReward(ri);
+        if (transformer->getNumberRewards() == 3) {
+            const float mid = result.getReward(2) / 2.0f;
+            s += mid;
+        }
+        if (s > 1.0) s = 1.0f;
+        else if (s < 0.0) s = 0.0f;
+        node->setFinalScore(ri, s);
+        node->setCurrentScore(ri, node->getFinalScore(ri, true));
+    }
+}
+
+}  // namespace gz

@@ -1,0 +1,76 @@
+"""NeuralNetwork wrapper (reference src/ggpzero/nn/network.py:10-165) whose model runs on the
+MI355X fused HIP forward.  ``get_model().predict_on_batch(X)`` keeps the Keras contract used by
+the poll loop (cppinterface.py:119): X float32 [N, C, H, W] -> [policy_0 .. policy_{R-1}, value]."""
+import numpy as np
+
+from .._native import HipNet
+from .desc import NetDesc
+from .weights import to_blob
+
+
+def desc_from_conf(nn_model_conf, generation_descr=None):
+    """NNModelConfig (+ GenerationDescription.draw_head) -> NetDesc.  v1 topology only."""
+    c = nn_model_conf
+    if c.resnet_v2 or c.squeeze_excite_layers or c.global_pooling_value or c.concat_all_layers:
+        raise NotImplementedError("only the v1 residual topology (resnet_v2=False) has a HIP forward")
+    draw = bool(generation_descr is not None and generation_descr.draw_head)
+    return NetDesc(input_channels=c.input_channels, input_columns=c.input_columns, input_rows=c.input_rows,
+                   cnn_filter_size=c.cnn_filter_size, residual_layers=c.residual_layers,
+                   policy_dist_count=list(c.policy_dist_count), value_hidden_size=c.value_hidden_size,
+                   num_values=3 if draw else 2, cnn_kernel_size=c.cnn_kernel_size, leaky_relu=c.leaky_relu)
+
+
+class HipModel(object):
+    """Model object with the Keras inference surface the hot path uses."""
+
+    def __init__(self, desc, weights, device=0):
+        self.desc = desc
+        self.weights = weights
+        self.net = HipNet(desc, device)
+        self.net.set_weights(to_blob(weights))
+
+    def predict_on_batch(self, X):
+        X = np.asarray(X, dtype=np.float32)
+        d = self.desc
+        assert X.shape[1:] == (d.input_channels, d.input_columns, d.input_rows), X.shape
+        return self.net.forward(X)
+
+    def predict(self, X, batch_size=None):
+        return self.predict_on_batch(X)
+
+    def set_weights(self, weights):
+        self.weights = weights
+        self.net.set_weights(to_blob(weights))
+
+    def last_kernel_ms(self):
+        return self.net.last_kernel_ms()
+
+
+class HeadResult(object):
+    def __init__(self, transformer, policies, values):
+        assert len(transformer.policy_dist_count) == len(policies)
+        self.policies = policies
+        self.scores = values
+
+
+class NeuralNetwork(object):
+    def __init__(self, gdl_bases_transformer, model, generation_descr):
+        self.gdl_bases_transformer = gdl_bases_transformer
+        self.model = model
+        self.generation_descr = generation_descr
+
+    def get_model(self):
+        return self.model
+
+    def predict_n(self, states, prev_states=None):
+        to_channels = self.gdl_bases_transformer.state_to_channels
+        if prev_states:
+            X = np.array([to_channels(s, p) for s, p in zip(states, prev_states)])
+        else:
+            X = np.array([to_channels(s) for s in states])
+        Y = self.model.predict_on_batch(X)
+        return [HeadResult(self.gdl_bases_transformer, [Y[k][i] for k in range(len(Y) - 1)], Y[-1][i])
+                for i in range(len(states))]
+
+    def predict_1(self, state, prev_states=None):
+        return self.predict_n([state], [prev_states] if prev_states else None)[0]

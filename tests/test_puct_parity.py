@@ -1,0 +1,141 @@
+"""Bit-exact parity of the native PUCT / self-play engine (libgz_engine.so through the reference's
+poll protocol) with the oracle restatement (oracle/puct_ref.py): identical planes at every poll,
+identical samples (policies, visits, scores, match ids) and identical root visit counts, given the
+same network outputs.  Small cases only (the oracle is pure Python)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from galvanise_zero_amd import cppinterface
+from galvanise_zero_amd.defs import templates
+from puct_harness import Setup, run_native_supervisor, run_oracle_supervisor, sample_key
+from oracle import games_ref
+from oracle import puct_ref as P
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _selfplay_conf(evals, noise, backup_finalised, abort=-1):
+    conf = templates.selfplay_config_template()
+    conf.evals_per_move = evals
+    conf.puct_config.dirichlet_noise_pct = noise
+    conf.puct_config.backup_finalised = backup_finalised
+    conf.run_to_end_puct_config.dirichlet_noise_pct = noise if noise < 0 else 0.15
+    conf.run_to_end_puct_config.backup_finalised = backup_finalised
+    conf.abort_max_length = abort
+    return conf
+
+
+@pytest.fixture(scope="module")
+def small():
+    return Setup("breakthroughSmall")
+
+
+@pytest.mark.parametrize("noise,bf,abort,seed", [(-1, True, -1, 3), (0.25, True, -1, 4), (0.25, False, 10, 5)])
+def test_supervisor_selfplay_parity(small, noise, bf, abort, seed):
+    conf = _selfplay_conf(20, noise, bf, abort)
+    polls = 1500
+    nlog, nsamples, nstats, _ = run_native_supervisor(small, conf, 4, polls, seed=seed)
+    olog, osamples, man = run_oracle_supervisor(small, conf, 4, polls, seed=seed, native_log=nlog)
+    assert len(nlog) == len(olog) == polls
+    a = [sample_key(small, s, True) for s in nsamples]
+    b = [sample_key(small, s, False) for s in osamples]
+    assert a == b
+    if abort < 0:
+        assert len(a) > 20
+    assert nstats["evaluations"] == sum(x.shape[0] for x in nlog[:-1]) // (small.transformer.num_channels *
+                                                                          small.transformer.channel_size)
+
+
+def _player_run(setup, conf, evals, moves, seed):
+    """Play `moves` moves of PlayPoller vs the oracle Player from the initial state; returns the
+    per-move root (move, traversals, policy_prob) lists of both."""
+    ct = cppinterface.create_c_transformer(setup.transformer)
+    cp = cppinterface._CPlayer(setup.sm, ct, conf, seed=seed)
+    op = P.Player(setup.ref_sm, setup.ref_planes, conf, list(setup.transformer.policy_dist_count),
+                  setup.transformer.num_rewards, setup.num_prev_states, seed=seed)
+    cp.player_reset(0)
+    op.reset(0)
+    words = setup.sm.get_initial_state()
+    out_n, out_o = [], []
+    for m in range(moves):
+        state = games_ref.words_to_state(words)
+        cp.player_move(words, evals)
+        op.move(state, evals)
+        arrays = setup.empty_arrays()
+        pred = (0, arrays[:-1], arrays[-1])
+        while True:
+            bn = cp.poll(len(arrays[0]), arrays)
+            bo = op.poll(*pred)
+            if bn is None or bo is None:
+                assert bn is None and bo is None
+                break
+            assert np.array_equal(np.array(bn), bo)
+            arrays = setup.nn(np.array(bn))
+            pred = (arrays[0].shape[0], arrays[:-1], arrays[-1])
+        sm = setup.sm
+        sm.update_bases(words)
+        lead = 0 if len(sm.get_legal_state(0)) > 1 else 1
+        gn = cp.player_get_move(lead)
+        go = op.get_move(lead)
+        assert gn[0] == go[0] and gn[2] == go[2] and abs(gn[1] - go[1]) == 0
+        rn, ro = cp.root_children(), op.root_children()
+        assert [(a, t) for a, t, _ in rn] == [(a, t) for a, t, _ in ro]
+        assert [np.float32(p) for _, _, p in rn] == [np.float32(p) for _, _, p in ro]
+        out_n.append(rn)
+        joint = [gn[0] if r == lead else 0 for r in range(2)]
+        cp.player_apply_move(joint)
+        op.apply_move(tuple(joint))
+        # drive the apply_move coroutines (no evaluation normally needed)
+        arrays = setup.empty_arrays()
+        pred = (0, arrays[:-1], arrays[-1])
+        while True:
+            bn = cp.poll(0, arrays)
+            bo = op.poll(*pred)
+            if bn is None or bo is None:
+                assert bn is None and bo is None
+                break
+            arrays = setup.nn(np.array(bn))
+            bo2 = op.poll(arrays[0].shape[0], arrays[:-1], arrays[-1])
+        words = sm.next_state(joint)
+        sm.update_bases(words)
+        if sm.is_terminal():
+            break
+    return out_n
+
+
+@pytest.mark.parametrize("game,batch,choose,evals", [("breakthroughSmall", 1, "choose_top_visits", 60),
+                                                     ("breakthroughSmall", 8, "choose_top_visits", 150),
+                                                     ("breakthrough", 1, "choose_temperature", 40)])
+def test_player_visit_counts_bit_exact(game, batch, choose, evals):
+    setup = Setup(game)
+    conf = templates.base_puct_config(batch_size=batch, choose=choose, dirichlet_noise_pct=0.25,
+                                      think_time=-1, converged_visits=1)
+    visits = _player_run(setup, conf, evals, 4, seed=9)
+    assert sum(t for _, t, _ in visits[0]) > evals // 2
+
+
+def test_player_golden_visits():
+    """Frozen root visit counts (tests/golden/puct_player.json, made by tests/golden/make_puct_golden.py)."""
+    g = json.load(open(os.path.join(GOLDEN, "puct_player.json")))
+    setup = Setup(g["game"])
+    conf = templates.base_puct_config(**g["conf"])
+    visits = _player_run(setup, conf, g["evals"], g["moves"], seed=g["seed"])
+    assert [[list(x[:2]) for x in mv] for mv in visits] == g["root_visits"]
+
+
+def test_workers_deterministic(small):
+    """Two worker threads (2 pools each): per-pool RNG streams + per-pool duplicate filter make the
+    sample set independent of thread interleaving."""
+    conf = _selfplay_conf(16, 0.25, True)
+    runs = []
+    for _ in range(2):
+        _, samples, stats, keep = run_native_supervisor(small, conf, 3, 1200, seed=21, workers=2)
+        # samples are collected every poll; flush what remains
+        sup = keep[0]
+        samples = samples + (sup.fetch_samples() or [])
+        runs.append(sorted((s["match_identifier"], s["depth"], json.dumps(s["policies"])) for s in samples))
+        del keep
+    assert runs[0] == runs[1] and len(runs[0]) > 0
