@@ -1,0 +1,210 @@
+"""Benchmark: self-play games/sec + NN leaf-evals/sec, breakthrough 8x8 @ 800 playouts/move
+(BASELINE.json configs[1]: 6-block x 128-filter net, eval batch 256), on N GPUs of one node.
+
+One process per GPU (torchrun for N>1).  Each rank runs the native self-play runner on its GPU:
+T host threads x P game pools x 256 games, one HIP stream per pool, the fused HIP forward per
+batch.  Games shard across ranks by global game index (no data-path collective); RCCL is used only
+to broadcast the weight blob from rank 0 (the generation-roll hook) before timing.
+
+A "step" = one NN batch (256 leaf evaluations) on every pool of every rank.  W warmup steps, then
+exactly K timed steps bracketed by barrier + synchronize; the time is the max over ranks, `value` is
+whole-job leaf-evals/sec.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0      # gfx950 dense bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1500)
+    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--threads", type=int, default=0, help="host threads per GPU (0: auto)")
+    ap.add_argument("--pools", type=int, default=2, help="game pools per thread")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--evals", type=int, default=800)
+    ap.add_argument("--mode", choices=["template", "literal"], default="template")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=20251015)
+    return ap.parse_args()
+
+
+def selfplay_conf(mode, evals):
+    from galvanise_zero_amd.defs import templates
+    if mode == "literal":
+        return templates.literal_selfplay_config(evals)
+    conf = templates.selfplay_config_template()
+    conf.evals_per_move = evals
+    return conf
+
+
+def setup_game():
+    from galvanise_zero_amd.defs import templates
+    from galvanise_zero_amd.nn.bases import GdlBasesTransformer
+    from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS
+    from galvanise_zero_amd.sm import get_sm
+    cfg = BASELINE_CONFIGS[2]
+    sm = get_sm(cfg["game"])
+    gen = templates.default_generation_desc(cfg["game"], num_previous_states=1)
+    transformer = GdlBasesTransformer(sm, gen)
+    desc = cfg["desc"]
+    assert (transformer.num_channels, transformer.num_cols, transformer.num_rows) == \
+        (desc.input_channels, desc.input_columns, desc.input_rows)
+    return sm, transformer, desc
+
+
+def cpu_baseline(seconds, evals, mode, batch):
+    """CPU restatement timed on the host: the same engine driven by the reference's Python poll
+    loop with the oracle's CPU forward (oracle/nn_ref.py) in place of the GPU."""
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+    from galvanise_zero_amd import cppinterface
+    from galvanise_zero_amd.nn.weights import random_weights
+    from oracle import nn_ref
+
+    sm, transformer, desc = setup_game()
+    weights = random_weights(desc, 7921)
+    cores = min(16, os.cpu_count() or 1)
+
+    class OracleModel(object):
+        def predict_on_batch(self, X):
+            return nn_ref.forward(desc, weights, X)
+
+    class NN(object):
+        gdl_bases_transformer = transformer
+
+        def get_model(self):
+            return OracleModel()
+
+    with threadpool_limits(limits=cores):
+        sup = cppinterface.Supervisor(sm, NN(), batch_size=batch, seed=1, per_pool_unique_states=True)
+        sup.start_self_play(selfplay_conf(mode, evals), 0)
+        t0 = time.time()
+        sup.poll(do_stats=True)
+        rows0 = sup.total_predictions
+        t0 = time.time()
+        while time.time() - t0 < seconds:
+            sup.poll(do_stats=True)
+        el = time.time() - t0
+        rows = sup.total_predictions - rows0
+    return {"value": rows / el, "unit": "leaf-evals/s", "cores": cores, "kind": "port",
+            "sample": "%.1f s of breakthrough self-play (%d games inline, batch %d, %d evals/move, %s mode): "
+                      "native engine + oracle fp64 numpy forward via the Python poll loop" %
+                      (el, batch, batch, evals, mode)}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from galvanise_zero_amd._native import HipNet
+    from galvanise_zero_amd.nn.weights import random_weights, to_blob
+    from galvanise_zero_amd.runner import SelfPlayRunner
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    sm, transformer, desc = setup_game()
+    net = HipNet(desc, local_rank)
+
+    # weights: rank 0 creates, RCCL broadcast of the blob (the only collective on the path)
+    blob = torch.empty(net.weight_count, dtype=torch.float32, device="cuda")
+    if rank == 0:
+        blob.copy_(torch.from_numpy(to_blob(random_weights(desc, 7921))))
+    if world > 1:
+        dist.broadcast(blob, src=0)
+    torch.cuda.synchronize()
+    net.set_weights_device(blob.data_ptr(), net.weight_count)
+
+    cpus = os.cpu_count() or 4
+    threads = args.threads or max(1, min(15, cpus // max(1, world) - 1))
+    runner = SelfPlayRunner(net, sm, transformer, selfplay_conf(args.mode, args.evals), device=local_rank,
+                            num_threads=threads, pools_per_thread=args.pools, batch_size=args.batch,
+                            seed=args.seed, game_index_base=rank * threads * args.pools * args.batch)
+    npools = runner.num_pools
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    runner.start()
+    runner.wait_batches(args.warmup * npools, timeout_s=3600)
+    barrier()
+    s0 = runner.stats()
+    t0 = time.perf_counter()
+    runner.wait_batches((args.warmup + args.steps) * npools, timeout_s=3600)
+    s1 = runner.stats()
+    t1 = time.perf_counter()
+    barrier()
+    t_end = time.perf_counter()
+    runner.stop()
+    elapsed = t1 - t0
+
+    d = {k: s1[k] - s0[k] for k in s1}
+    vec = torch.tensor([d["rows"], d["batches"], d["games_completed"], d["games_with_samples"], d["samples"],
+                        d["kernel_ms"], d["kernel_launches"], elapsed], dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(vec, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    rows, batches, games, games_s, samples, kms, launches, _ = vec.tolist()
+    T = tmax.item()
+
+    if rank == 0:
+        flops = desc.flops_per_eval()
+        avg_kernel_s = (kms / launches) / 1e3 if launches else float("nan")
+        rows_per_launch = rows / launches if launches else float("nan")
+        achieved = flops * rows_per_launch / avg_kernel_s / 1e12
+        out = {
+            "metric": "self-play games/sec + NN leaf-evals/sec, breakthrough 8x8 @ 800 playouts/move",
+            "value": rows / T,
+            "unit": "leaf-evals/s",
+            "games_per_sec": games / T,
+            "sample_games_per_sec": games_s / T,
+            "samples_per_sec": samples / T,
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * T / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic: self-play from the initial position, random-init weights (no .h5 in reference)",
+            "config": {"workload": "breakthrough 8x8 self-play, v1 6x128 net, %d evals/move (%s mode), eval "
+                                   "batch %d" % (args.evals, args.mode, args.batch),
+                       "games_per_gpu": npools * args.batch, "threads_per_gpu": threads,
+                       "pools_per_thread": args.pools, "eval_batch": args.batch, "parallelism": "games sharded dp%d" % world},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": None,
+                         "kernel": "gznn::forward_kernel<128,8,8>", "avg_kernel_ms": avg_kernel_s * 1e3,
+                         "rows_per_launch": rows_per_launch, "flop_per_leaf": flops},
+            "gpu_busy_frac": (kms / 1e3) / (T * world) if T > 0 else None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.evals, args.mode, args.batch)
+        print(json.dumps(out), flush=True)
+    runner.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -348,3 +348,38 @@ def make_selfplay_config(conf):
         v = _get(conf, name, default)
         setattr(c, name, int(v) if ctype is ctypes.c_int else float(v))
     return c
+
+
+###############################################################################
+# runner (libgz_nn.so, runner.hip)
+
+class GzRunnerConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("num_threads", ctypes.c_int), ("pools_per_thread", ctypes.c_int),
+                ("batch_size", ctypes.c_int), ("seed", ctypes.c_ulonglong), ("game_index_base", ctypes.c_long),
+                ("per_pool_unique_states", ctypes.c_int)]
+
+
+class GzRunnerStats(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_long), ("rows", ctypes.c_long), ("kernel_ms", ctypes.c_double),
+                ("kernel_launches", ctypes.c_long), ("games_completed", ctypes.c_long),
+                ("games_with_samples", ctypes.c_long), ("samples", ctypes.c_long), ("no_samples", ctypes.c_long),
+                ("resigns", ctypes.c_long), ("aborts", ctypes.c_long), ("dupes", ctypes.c_long)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+def runner_lib():
+    lib = nn_lib()
+    if not getattr(lib, "_gz_runner_typed", False):
+        lib.gz_runner_create.restype = _VP
+        lib.gz_runner_create.argtypes = [_VP, _VP, _VP, ctypes.POINTER(GzRunnerConfig),
+                                         ctypes.POINTER(GzSelfPlayConfig), _IP, ctypes.c_int, ctypes.c_int]
+        lib.gz_runner_start.argtypes = [_VP]
+        lib.gz_runner_wait_batches.argtypes = [_VP, ctypes.c_long, ctypes.c_double]
+        lib.gz_runner_stats_get.argtypes = [_VP, ctypes.POINTER(GzRunnerStats)]
+        lib.gz_runner_stop.argtypes = [_VP]
+        lib.gz_runner_destroy.argtypes = [_VP]
+        lib.gz_runner_last_error.restype = ctypes.c_char_p
+        lib._gz_runner_typed = True
+    return lib

@@ -71,6 +71,51 @@ double gz_net_flops_per_eval(const gz_net* net);
 
 const char* gz_nn_last_error(void);
 
+/* ---- native self-play driver (runner.hip) ----------------------------------------------------
+ * Replaces the Python poll loop of the reference (cppinterface.py:131-144 driven by
+ * distributed/worker.py:191) and its worker threads (supervisor.cpp:79-99,196-245) for the
+ * steady state: num_threads host threads x pools_per_thread game pools x batch_size games, one HIP
+ * stream per pool, planes / predictions in pinned host memory, the fused forward on the stream.
+ * Uses the engine C-ABI (include/gzero_engine.h) for the pools. */
+struct gz_sm;
+struct gz_transformer;
+struct gz_selfplay_config;
+typedef struct gz_runner gz_runner;
+
+typedef struct gz_runner_config {
+    int device;
+    int num_threads;
+    int pools_per_thread;
+    int batch_size;              /* games per pool = rows per NN batch */
+    unsigned long long seed;
+    long game_index_base;        /* global index of the first game (multi-GPU sharding) */
+    int per_pool_unique_states;  /* pools always own their duplicate filter here (deterministic) */
+} gz_runner_config;
+
+typedef struct gz_runner_stats {
+    long batches;                /* NN forwards completed */
+    long rows;                   /* leaf evaluations completed */
+    double kernel_ms;            /* summed forward-kernel device time (HIP events on pool streams) */
+    long kernel_launches;
+    long games_completed;
+    long games_with_samples;
+    long samples;
+    long no_samples;
+    long resigns;
+    long aborts;
+    long dupes;
+} gz_runner_stats;
+
+gz_runner* gz_runner_create(gz_net* net, const struct gz_sm* sm, const struct gz_transformer* t,
+                            const gz_runner_config* cfg, const struct gz_selfplay_config* conf,
+                            const int* policy_sizes, int num_policies, int num_values);
+int gz_runner_start(gz_runner* r);
+int gz_runner_wait_batches(gz_runner* r, long total_batches, double timeout_s);
+int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out);
+int gz_runner_stop(gz_runner* r);
+void gz_runner_destroy(gz_runner* r);
+const char* gz_runner_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif
