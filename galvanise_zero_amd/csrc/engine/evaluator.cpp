@@ -202,6 +202,226 @@ void PuctEvaluator::balanceFirstMoves(int max_moves) {
     }
 }
 
+// ---- order-independent fast paths -----------------------------------------------------------
+// The reference sorts the children (std::sort, unstable) before every selection / top-visits
+// choice.  Whenever the result provably does not depend on the order the sort produces -- no RNG is
+// drawn inside the loop, and the winning element is strictly separated from every other element
+// under the loop's own (float-truncating) comparison semantics -- a single unsorted pass returns
+// the identical child.  Otherwise the literal sorted path runs.  tests/test_puct_parity.py checks
+// the engine against the oracle (which always sorts); GZ_VERIFY_FASTPATH=1 cross-checks at run time.
+
+static bool verify_fastpath() {
+    static const bool v = [] {
+        const char* e = std::getenv("GZ_VERIFY_FASTPATH");
+        return e != nullptr && e[0] == '1';
+    }();
+    return v;
+}
+
+// comparator of sortedChildrenTraversals (node.cpp:356-369, next_probability=false)
+static inline bool travBefore(const PuctNodeChild* a, const PuctNodeChild* b) {
+    if (a->traversals == b->traversals) return a->policy_prob > b->policy_prob;
+    return a->traversals > b->traversals;
+}
+
+// comparator of sortedChildren (node.cpp:326-339, next_probability=false)
+static inline bool visitsBefore(const PuctNodeChild* a, const PuctNodeChild* b) {
+    const int va = a->to_node == nullptr ? 0 : a->to_node->visits;
+    const int vb = b->to_node == nullptr ? 0 : b->to_node->visits;
+    if (va == vb) return a->policy_prob > b->policy_prob;
+    return va > vb;
+}
+
+// Index of the unique first element under `before` among children with keep(i), or -1 if empty,
+// -2 if the first place is tied.
+template <typename Before, typename Keep>
+static int uniqueFirst(const PuctNode* node, Before before, Keep keep) {
+    int best = -1;
+    bool tied = false;
+    for (int i = 0; i < node->num_children; ++i) {
+        if (!keep(i)) continue;
+        const PuctNodeChild* c = node->getNodeChild(0, i);
+        if (best < 0) {
+            best = i;
+            continue;
+        }
+        const PuctNodeChild* b = node->getNodeChild(0, best);
+        if (before(c, b)) {
+            best = i;
+            tied = false;
+        } else if (!before(b, c)) {
+            tied = true;
+        }
+    }
+    return tied ? -2 : best;
+}
+
+// Second place (unique) after excluding `first`; -1 none, -2 tied (or not strictly after first).
+template <typename Before, typename Keep>
+static int uniqueSecond(const PuctNode* node, Before before, Keep keep, int first) {
+    const int s = uniqueFirst(node, before, [&](int i) { return i != first && keep(i); });
+    if (s >= 0 && !before(node->getNodeChild(0, first), node->getNodeChild(0, s))) return -2;
+    return s;
+}
+
+bool PuctEvaluator::chooseTopVisitsFast(const PuctNode* node, const PuctNodeChild** out) const {
+    const int ri = node->lead_role_index;
+    auto isWin = [&](int i) {
+        const PuctNodeChild* c = node->getNodeChild(0, i);
+        return c->to_node != nullptr && c->to_node->is_finalised && c->to_node->getCurrentScore(ri) > 0.99;
+    };
+    auto isLoss = [&](int i) {
+        const PuctNodeChild* c = node->getNodeChild(0, i);
+        return c->to_node != nullptr && c->to_node->is_finalised && !(c->to_node->getCurrentScore(ri) > 0.99) &&
+               c->to_node->getCurrentScore(ri) < 0.01;
+    };
+    bool any_win = false;
+    for (int i = 0; i < node->num_children && !any_win; ++i) any_win = isWin(i);
+    if (any_win) {
+        const int w = uniqueFirst(node, travBefore, isWin);
+        if (w < 0) return false;
+        *out = node->getNodeChild(0, w);
+        return true;
+    }
+    auto nonLoss = [&](int i) { return !isLoss(i); };
+    const int c0 = uniqueFirst(node, travBefore, nonLoss);
+    if (c0 == -2) return false;
+    int c1 = -1;
+    if (c0 >= 0) {
+        c1 = uniqueSecond(node, travBefore, nonLoss, c0);
+        if (c1 == -2) return false;
+    }
+    if (conf->top_visits_best_guess_converge_ratio > 0 && c0 >= 0 && c1 >= 0) {
+        const PuctNodeChild* a = node->getNodeChild(0, c0);
+        const PuctNodeChild* b = node->getNodeChild(0, c1);
+        if (a->to_node != nullptr && b->to_node != nullptr) {
+            if (b->traversals > a->traversals * conf->top_visits_best_guess_converge_ratio &&
+                b->to_node->getCurrentScore(ri) > a->to_node->getCurrentScore(ri))
+                *out = b;
+            else
+                *out = a;
+            return true;
+        }
+    }
+    const int first = uniqueFirst(node, travBefore, [](int) { return true; });
+    if (first < 0) return false;
+    *out = node->getNodeChild(0, first);
+    return true;
+}
+
+bool PuctEvaluator::convergedFast(int count, bool* out) const {
+    if (root->num_children < 2) {
+        *out = true;
+        return true;
+    }
+    auto all = [](int) { return true; };
+    const int i0 = uniqueFirst(root, visitsBefore, all);
+    if (i0 < 0) return false;
+    const int i1 = uniqueSecond(root, visitsBefore, all, i0);
+    if (i1 < 0) return false;
+    const PuctNode* n0 = root->getNodeChild(0, i0)->to_node;
+    const PuctNode* n1 = root->getNodeChild(0, i1)->to_node;
+    bool r = false;
+    if (n0 != nullptr && n1 != nullptr) {
+        const int role_index = root->lead_role_index;
+        r = n0->getCurrentScore(role_index) > n1->getCurrentScore(role_index) && n0->visits > n1->visits + count;
+    }
+    *out = r;
+    return true;
+}
+
+// Unsorted selection; returns false when the literal sorted loop must run instead.
+bool PuctEvaluator::selectChildFast(PuctNode* node, int depth, float prior_score, double sqrt_node_visits,
+                                    PuctNodeChild** out) {
+    if (node->visits > 1000 && node->visits < 40000000 && depth == 0) return false;   // root latch draws RNG
+    const int lead = node->lead_role_index;
+    int win = -1;
+    bool win_tied = false;
+    float win_key = 0.f;
+    int best = -1;
+    double best_score = 0.0;
+    for (int i = 0; i < node->num_children; ++i) {
+        PuctNodeChild* c = node->getNodeChild(0, i);
+        if (c->unselectable) continue;
+        if (c->to_node != nullptr && c->to_node->num_children > 0 &&
+            c->to_node->unselectable_count == c->to_node->num_children)
+            continue;
+        double child_score = prior_score;
+        const int traversals = c->traversals + 1;
+        const double inflight_visits = c->to_node != nullptr ? c->to_node->inflight_visits : 0;
+        if (c->traversals > 0 && inflight_visits > 0) return false;                  // discount draws RNG
+        double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
+                                   (traversals + inflight_visits);
+        if (c->to_node != nullptr) {
+            PuctNode* cn = c->to_node;
+            child_score = cn->getCurrentScore(lead);
+            if (cn->is_finalised) {
+                if (child_score > 0.99) {
+                    if (depth > 0) {
+                        // first win in sortedChildrenSelect order = highest current score
+                        const float k = cn->getCurrentScore(lead);
+                        if (win < 0 || k > win_key) {
+                            win = i;
+                            win_key = k;
+                            win_tied = false;
+                        } else if (k == win_key) {
+                            win_tied = true;
+                        }
+                        continue;
+                    }
+                    child_score *= 1.0f + node->puct_constant;
+                } else if (child_score < 0.01) {
+                    continue;   // bad_fallback candidate
+                } else {
+                    exploration_score = 0.0;
+                }
+            }
+        }
+        const double score = child_score + exploration_score;
+        if (best < 0 || score > best_score) {
+            best = i;
+            best_score = score;
+        }
+    }
+    if (win >= 0) {
+        if (win_tied) return false;
+        *out = node->getNodeChild(0, win);
+        return true;
+    }
+    if (best < 0) return false;   // nothing selectable: yields / fallbacks of the literal loop
+    // order independence of `if (score > best_score_float)` with best_score_float = (float)score:
+    // the max m must replace any incumbent and never be replaced.
+    const double fm = (float)best_score;
+    if (!(best_score > -1.0)) return false;
+    for (int i = 0; i < node->num_children; ++i) {
+        if (i == best) continue;
+        PuctNodeChild* c = node->getNodeChild(0, i);
+        if (c->unselectable) continue;
+        if (c->to_node != nullptr && c->to_node->num_children > 0 &&
+            c->to_node->unselectable_count == c->to_node->num_children)
+            continue;
+        double child_score = prior_score;
+        const int traversals = c->traversals + 1;
+        const double inflight_visits = c->to_node != nullptr ? c->to_node->inflight_visits : 0;
+        double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
+                                   (traversals + inflight_visits);
+        if (c->to_node != nullptr) {
+            PuctNode* cn = c->to_node;
+            child_score = cn->getCurrentScore(lead);
+            if (cn->is_finalised) {
+                if (child_score > 0.99) child_score *= 1.0f + node->puct_constant;
+                else if (child_score < 0.01) continue;
+                else exploration_score = 0.0;
+            }
+        }
+        const double sc = child_score + exploration_score;
+        if (sc > fm) return false;                       // c would replace m
+        if (!(best_score > (double)(float)sc)) return false;   // m would not replace c
+    }
+    *out = node->getNodeChild(0, best);
+    return true;
+}
+
 // evaluator.cpp:341-517
 PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
     GZ_ASSERT(!node->isTerminal());
@@ -218,6 +438,13 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
 
     const float prior_score = priorScore(node, depth);
     const double sqrt_node_visits = std::sqrt(node->visits + 1);
+
+    PuctNodeChild* fast_choice = nullptr;
+    const bool fast_ok = selectChildFast(node, depth, prior_score, sqrt_node_visits, &fast_choice);
+    if (fast_ok && !verify_fastpath()) {
+        path.emplace_back(node, fast_choice, fast_choice);
+        return fast_choice;
+    }
 
     float best_score = -1;
     PuctNodeChild* best_child = nullptr;
@@ -251,6 +478,10 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
             if (cn->is_finalised) {
                 if (child_score > 0.99) {
                     if (depth > 0) {
+                        if (fast_ok && c != fast_choice) {
+                            std::fprintf(stderr, "gz fast-path selectChild (win) mismatch\n");
+                            std::abort();
+                        }
                         path.emplace_back(node, c, c);
                         return c;
                     }
@@ -305,6 +536,10 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
         }
     }
     if (best_child_score == nullptr) best_child_score = best_child;
+    if (fast_ok && best_child != fast_choice) {
+        std::fprintf(stderr, "gz fast-path selectChild mismatch\n");
+        std::abort();
+    }
     if (best_child != nullptr) path.emplace_back(node, best_child, best_child_score);
     return best_child;
 }
@@ -583,6 +818,20 @@ const PuctNodeChild* PuctEvaluator::onNextMove(int max_evaluations, double end_t
 // evaluator.cpp:1100-1159
 const PuctNodeChild* PuctEvaluator::chooseTopVisits(const PuctNode* node) const {
     GZ_ASSERT(node != nullptr);
+    const PuctNodeChild* fast = nullptr;
+    if (chooseTopVisitsFast(node, &fast)) {
+        if (!verify_fastpath()) return fast;
+        const PuctNodeChild* exact = chooseTopVisitsExact(node);
+        if (exact != fast) {
+            std::fprintf(stderr, "gz fast-path chooseTopVisits mismatch\n");
+            std::abort();
+        }
+        return fast;
+    }
+    return chooseTopVisitsExact(node);
+}
+
+const PuctNodeChild* PuctEvaluator::chooseTopVisitsExact(const PuctNode* node) const {
     Children children = PuctNode::sortedChildrenTraversals(node);
     GZ_ASSERT(!children.empty());
     const int role_index = node->lead_role_index;
@@ -705,6 +954,18 @@ const PuctNodeChild* PuctEvaluator::choose(const PuctNode* node) {
 
 // evaluator.cpp:1342-1362
 bool PuctEvaluator::converged(int count) const {
+    bool fast = false;
+    if (convergedFast(count, &fast)) {
+        if (verify_fastpath() && convergedExact(count) != fast) {
+            std::fprintf(stderr, "gz fast-path converged mismatch\n");
+            std::abort();
+        }
+        return fast;
+    }
+    return convergedExact(count);
+}
+
+bool PuctEvaluator::convergedExact(int count) const {
     Children children = PuctNode::sortedChildren(root);
     if (children.size() >= 2) {
         PuctNode* n0 = children[0]->to_node;

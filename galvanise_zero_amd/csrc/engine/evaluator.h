@@ -86,6 +86,11 @@ private:
     PuctNode* lookupNode(const uint64_t* bs, int depth);
     PuctNode* createNode(PuctNode* parent, const uint64_t* state);
     PuctNodeChild* selectChild(PuctNode* node, Path& path);
+    bool selectChildFast(PuctNode* node, int depth, float prior_score, double sqrt_node_visits, PuctNodeChild** out);
+    bool chooseTopVisitsFast(const PuctNode* node, const PuctNodeChild** out) const;
+    const PuctNodeChild* chooseTopVisitsExact(const PuctNode* node) const;
+    bool convergedFast(int count, bool* out) const;
+    bool convergedExact(int count) const;
     void backup(float* new_scores, const Path& path);
     int treePlayout(PuctNode* current, Path& path);
     void playoutWorker(int worker_id);

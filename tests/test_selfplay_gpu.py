@@ -36,7 +36,8 @@ def test_dropin_supervisor_gpu_matches_oracle(hip_device):
     setup = Setup("breakthroughSmall")
     model = RecordingModel(HipModel(setup.desc, setup.weights, hip_device))
     nn = NeuralNetwork(setup.transformer, model, None)
-    sup = cppinterface.Supervisor(setup.sm, nn, batch_size=4, seed=7, per_pool_unique_states=True)
+    sup = cppinterface.Supervisor(setup.sm, nn, batch_size=4, seed=7, per_pool_unique_states=True,
+                                  identifier="t")
     sup.c_supervisor.set_sample_interval(1)
     conf = _conf()
     sup.start_self_play(conf, 0)
@@ -48,8 +49,6 @@ def test_dropin_supervisor_gpu_matches_oracle(hip_device):
     # oracle replay with the GPU's outputs
     outs = iter(model.outs)
 
-    class Replay(object):
-        pass
     setup.nn = lambda planes: next(outs)
     olog, osamples, _ = run_oracle_supervisor(setup, conf, 4, polls, seed=7, native_log=model.planes)
     assert len(olog) == polls
@@ -67,10 +66,10 @@ def test_native_runner_runs(hip_device):
     r = SelfPlayRunner(net, setup.sm, setup.transformer, _conf(), device=hip_device, num_threads=2,
                        pools_per_thread=2, batch_size=32, seed=3)
     r.start()
-    r.wait_batches(400, timeout_s=120)
+    r.wait_batches(4000, timeout_s=240)
     r.stop()
     st = r.stats()
     r.close()
-    assert st["batches"] >= 400 and st["rows"] > 0
+    assert st["batches"] >= 4000 and st["rows"] > 0
     assert st["kernel_launches"] == st["batches"] and st["kernel_ms"] > 0
     assert st["games_completed"] > 0
