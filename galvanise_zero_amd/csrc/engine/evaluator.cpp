@@ -265,35 +265,62 @@ static int uniqueSecond(const PuctNode* node, Before before, Keep keep, int firs
 }
 
 bool PuctEvaluator::chooseTopVisitsFast(const PuctNode* node, const PuctNodeChild** out) const {
+    // one pass: first win, first two non-losses and first overall under travBefore, with tie flags
     const int ri = node->lead_role_index;
-    auto isWin = [&](int i) {
-        const PuctNodeChild* c = node->getNodeChild(0, i);
-        return c->to_node != nullptr && c->to_node->is_finalised && c->to_node->getCurrentScore(ri) > 0.99;
-    };
-    auto isLoss = [&](int i) {
-        const PuctNodeChild* c = node->getNodeChild(0, i);
-        return c->to_node != nullptr && c->to_node->is_finalised && !(c->to_node->getCurrentScore(ri) > 0.99) &&
-               c->to_node->getCurrentScore(ri) < 0.01;
-    };
-    bool any_win = false;
-    for (int i = 0; i < node->num_children && !any_win; ++i) any_win = isWin(i);
-    if (any_win) {
-        const int w = uniqueFirst(node, travBefore, isWin);
-        if (w < 0) return false;
-        *out = node->getNodeChild(0, w);
+    const PuctNodeChild *w = nullptr, *a = nullptr, *b = nullptr, *f = nullptr;
+    bool w_tie = false, f_tie = false;
+    int a_n = 0, b_n = 0;
+    const PuctNodeChild* cs = node->children();
+    for (int i = 0; i < node->num_children; ++i) {
+        const PuctNodeChild* c = cs + i;
+        bool win = false, loss = false;
+        if (c->to_node != nullptr && c->to_node->is_finalised) {
+            const Score sc = c->to_node->getCurrentScore(ri);
+            win = sc > 0.99;
+            loss = !win && sc < 0.01;
+        }
+        // overall first
+        if (f == nullptr || travBefore(c, f)) {
+            f = c;
+            f_tie = false;
+        } else if (!travBefore(f, c)) {
+            f_tie = true;
+        }
+        if (win) {
+            if (w == nullptr || travBefore(c, w)) {
+                w = c;
+                w_tie = false;
+            } else if (!travBefore(w, c)) {
+                w_tie = true;
+            }
+        }
+        if (!loss) {
+            // top-2 with multiplicities: a (a_n equivalent elements), then b (b_n equivalent)
+            if (a == nullptr) {
+                a = c;
+                a_n = 1;
+            } else if (travBefore(c, a)) {
+                b = a;
+                b_n = a_n;
+                a = c;
+                a_n = 1;
+            } else if (!travBefore(a, c)) {
+                a_n++;
+            } else if (b == nullptr || travBefore(c, b)) {
+                b = c;
+                b_n = 1;
+            } else if (!travBefore(b, c)) {
+                b_n++;
+            }
+        }
+    }
+    if (w != nullptr) {
+        if (w_tie) return false;
+        *out = w;
         return true;
     }
-    auto nonLoss = [&](int i) { return !isLoss(i); };
-    const int c0 = uniqueFirst(node, travBefore, nonLoss);
-    if (c0 == -2) return false;
-    int c1 = -1;
-    if (c0 >= 0) {
-        c1 = uniqueSecond(node, travBefore, nonLoss, c0);
-        if (c1 == -2) return false;
-    }
-    if (conf->top_visits_best_guess_converge_ratio > 0 && c0 >= 0 && c1 >= 0) {
-        const PuctNodeChild* a = node->getNodeChild(0, c0);
-        const PuctNodeChild* b = node->getNodeChild(0, c1);
+    if (a_n > 1 || b_n > 1) return false;   // the first two non-loss places are not unique
+    if (conf->top_visits_best_guess_converge_ratio > 0 && a != nullptr && b != nullptr) {
         if (a->to_node != nullptr && b->to_node != nullptr) {
             if (b->traversals > a->traversals * conf->top_visits_best_guess_converge_ratio &&
                 b->to_node->getCurrentScore(ri) > a->to_node->getCurrentScore(ri))
@@ -303,9 +330,8 @@ bool PuctEvaluator::chooseTopVisitsFast(const PuctNode* node, const PuctNodeChil
             return true;
         }
     }
-    const int first = uniqueFirst(node, travBefore, [](int) { return true; });
-    if (first < 0) return false;
-    *out = node->getNodeChild(0, first);
+    if (f == nullptr || f_tie) return false;
+    *out = f;
     return true;
 }
 
@@ -334,31 +360,34 @@ bool PuctEvaluator::convergedFast(int count, bool* out) const {
 bool PuctEvaluator::selectChildFast(PuctNode* node, int depth, float prior_score, double sqrt_node_visits,
                                     PuctNodeChild** out) {
     if (node->visits > 1000 && node->visits < 40000000 && depth == 0) return false;   // root latch draws RNG
+    const int n = node->num_children;
+    if (n > 512) return false;
+    double scores[512];
     const int lead = node->lead_role_index;
     int win = -1;
     bool win_tied = false;
     float win_key = 0.f;
     int best = -1;
     double best_score = 0.0;
-    for (int i = 0; i < node->num_children; ++i) {
-        PuctNodeChild* c = node->getNodeChild(0, i);
+    PuctNodeChild* cs = node->children();
+    for (int i = 0; i < n; ++i) {
+        PuctNodeChild* c = cs + i;
+        scores[i] = -1e300;    // not a candidate
         if (c->unselectable) continue;
-        if (c->to_node != nullptr && c->to_node->num_children > 0 &&
-            c->to_node->unselectable_count == c->to_node->num_children)
-            continue;
+        const PuctNode* cn = c->to_node;
+        if (cn != nullptr && cn->num_children > 0 && cn->unselectable_count == cn->num_children) continue;
         double child_score = prior_score;
         const int traversals = c->traversals + 1;
-        const double inflight_visits = c->to_node != nullptr ? c->to_node->inflight_visits : 0;
+        const double inflight_visits = cn != nullptr ? cn->inflight_visits : 0;
         if (c->traversals > 0 && inflight_visits > 0) return false;                  // discount draws RNG
         double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
                                    (traversals + inflight_visits);
-        if (c->to_node != nullptr) {
-            PuctNode* cn = c->to_node;
+        if (cn != nullptr) {
             child_score = cn->getCurrentScore(lead);
             if (cn->is_finalised) {
                 if (child_score > 0.99) {
                     if (depth > 0) {
-                        // first win in sortedChildrenSelect order = highest current score
+                        // the first win in sortedChildrenSelect order has the highest current score
                         const float k = cn->getCurrentScore(lead);
                         if (win < 0 || k > win_key) {
                             win = i;
@@ -378,6 +407,7 @@ bool PuctEvaluator::selectChildFast(PuctNode* node, int depth, float prior_score
             }
         }
         const double score = child_score + exploration_score;
+        scores[i] = score;
         if (best < 0 || score > best_score) {
             best = i;
             best_score = score;
@@ -385,40 +415,19 @@ bool PuctEvaluator::selectChildFast(PuctNode* node, int depth, float prior_score
     }
     if (win >= 0) {
         if (win_tied) return false;
-        *out = node->getNodeChild(0, win);
+        *out = cs + win;
         return true;
     }
-    if (best < 0) return false;   // nothing selectable: yields / fallbacks of the literal loop
-    // order independence of `if (score > best_score_float)` with best_score_float = (float)score:
-    // the max m must replace any incumbent and never be replaced.
+    if (best < 0 || !(best_score > -1.0)) return false;
+    // order independence of `if (score > best_score_float)`: the max m must replace any incumbent
+    // (m > float(c)) and never be replaced (c <= float(m)).
     const double fm = (float)best_score;
-    if (!(best_score > -1.0)) return false;
-    for (int i = 0; i < node->num_children; ++i) {
-        if (i == best) continue;
-        PuctNodeChild* c = node->getNodeChild(0, i);
-        if (c->unselectable) continue;
-        if (c->to_node != nullptr && c->to_node->num_children > 0 &&
-            c->to_node->unselectable_count == c->to_node->num_children)
-            continue;
-        double child_score = prior_score;
-        const int traversals = c->traversals + 1;
-        const double inflight_visits = c->to_node != nullptr ? c->to_node->inflight_visits : 0;
-        double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
-                                   (traversals + inflight_visits);
-        if (c->to_node != nullptr) {
-            PuctNode* cn = c->to_node;
-            child_score = cn->getCurrentScore(lead);
-            if (cn->is_finalised) {
-                if (child_score > 0.99) child_score *= 1.0f + node->puct_constant;
-                else if (child_score < 0.01) continue;
-                else exploration_score = 0.0;
-            }
-        }
-        const double sc = child_score + exploration_score;
-        if (sc > fm) return false;                       // c would replace m
-        if (!(best_score > (double)(float)sc)) return false;   // m would not replace c
+    for (int i = 0; i < n; ++i) {
+        if (i == best || scores[i] == -1e300) continue;
+        const double sc = scores[i];
+        if (sc > fm || !(best_score > (double)(float)sc)) return false;
     }
-    *out = node->getNodeChild(0, best);
+    *out = cs + best;
     return true;
 }
 

@@ -21,6 +21,8 @@ public:
     void addBoardBase(int base_indx, int buf_incr) {
         board_space.push_back({base_indx, buf_incr});
         interested.insert(base_indx);
+        if ((int)board_offset.size() <= base_indx) board_offset.resize(base_indx + 1, -1);
+        board_offset[base_indx] = buf_incr;
     }
     void addControlBase(int base_indx, int channel_id, float value) {
         control_space.push_back({base_indx, channel_id, value});
@@ -55,6 +57,7 @@ private:
     const int channel_size, channels_per_state, num_control_channels, num_prev_states, num_rewards;
     std::vector<int> expected_policy_sizes;
     std::vector<BoardBase> board_space;
+    std::vector<int> board_offset;     // base index -> buffer offset (-1: not a board base)
     std::vector<ControlBase> control_space;
     std::set<int> interested;
 };
