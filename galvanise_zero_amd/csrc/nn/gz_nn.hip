@@ -8,7 +8,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -37,6 +39,7 @@ struct gz_net {
     size_t nweights = 0;
     int smem = 0;
     const void* kfn = nullptr;
+    int nb = 1;                    // boards per workgroup of the selected kernel variant
     bool has_weights = false;
 
     char* dmem = nullptr;          // all weights, one allocation
@@ -52,23 +55,57 @@ struct gz_net {
 extern "C" const char* gz_nn_last_error(void) { return g_err.c_str(); }
 
 // ---- kernel instantiations ----------------------------------------------------------------
-template <int F, int H, int W>
-static const void* kernel_for() {
-    return (const void*)&forward_kernel<F, H, W>;
+// Variants: NB = boards per workgroup (weight-fragment reuse factor), WPE = minimum resident
+// waves per SIMD the register budget must allow (= workgroups per CU).  The default per geometry
+// is the measured fastest ("forward kernel"); GZ_KERNEL_VARIANT=<NB><WPE> (e.g. "22")
+// overrides it for experiments.
+struct KernelChoice {
+    const void* fn = nullptr;
+    int act_bytes = 0;
+    int nb = 1;
+};
+
+template <int F, int H, int W, int NB, int WPE>
+static KernelChoice kernel_for() {
+    KernelChoice k;
+    k.fn = (const void*)&forward_kernel<F, H, W, NB, WPE>;
+    k.act_bytes = Geo<F, H, W, NB>::ACT_BYTES;
+    k.nb = NB;
+    return k;
 }
 
-static const void* select_kernel(int F, int H, int W, int* act_bytes) {
-#define GZ_CASE(F_, H_, W_)                                            \
-    if (F == F_ && H == H_ && W == W_) {                               \
-        *act_bytes = Geo<F_, H_, W_>::ACT_BYTES;                       \
-        return kernel_for<F_, H_, W_>();                               \
+template <int F, int H, int W>
+static KernelChoice variants(int v) {
+    switch (v) {
+        case 11: return kernel_for<F, H, W, 1, 1>();
+        case 12: return kernel_for<F, H, W, 1, 2>();
+        case 13: return kernel_for<F, H, W, 1, 3>();
+        case 14: return kernel_for<F, H, W, 1, 4>();
+        case 21: return kernel_for<F, H, W, 2, 1>();
+        case 22: return kernel_for<F, H, W, 2, 2>();
+        case 41: return kernel_for<F, H, W, 4, 1>();
+        default: return KernelChoice{};
     }
+}
+
+static int default_variant(int F, int H, int W) {
+    // measured on MI355X (profiles/r01_kernel_variants.txt): 3 workgroups/CU wins on 128x8x8,
+    // 2 elsewhere; 2 boards per workgroup only pays at batches >= 1024
+    if (F == 128 && H == 8 && W == 8) return 13;
+    return 12;
+}
+
+static KernelChoice select_kernel(int F, int H, int W) {
+    int v = default_variant(F, H, W);
+    if (const char* e = getenv("GZ_KERNEL_VARIANT")) v = atoi(e);
+#define GZ_CASE(F_, H_, W_) \
+    if (F == F_ && H == H_ && W == W_) return variants<F_, H_, W_>(v);
     GZ_CASE(64, 6, 6)
     GZ_CASE(128, 6, 6)
     GZ_CASE(64, 8, 8)
     GZ_CASE(128, 8, 8)
 #undef GZ_CASE
-    return nullptr;
+    return KernelChoice{};
 }
 
 // ---- bf16 (round to nearest even) -------------------------------------------------------------
@@ -96,8 +133,8 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     if (d.cnn_kernel_size != 3) { fail("only cnn_kernel_size 3 is supported"); return nullptr; }
     if (d.role_count < 1 || d.role_count > GZ_MAX_ROLES) { fail("role_count out of range"); return nullptr; }
     if (d.num_values < 1 || d.num_values > 4) { fail("num_values out of range"); return nullptr; }
-    int act_bytes = 0;
-    const void* k = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, &act_bytes);
+    const KernelChoice kc = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows);
+    const void* k = kc.fn;
     if (!k) {
         fail("unsupported network geometry F=" + std::to_string(d.cnn_filter_size) + " H=" +
              std::to_string(d.input_columns) + " W=" + std::to_string(d.input_rows));
@@ -107,13 +144,16 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     net->d = d;
     net->device = device;
     net->kfn = k;
+    net->nb = kc.nb;
     net->K0 = ((9 * d.input_channels + 31) / 32) * 32;
     net->nweights = spec_count(d);
     int maxP = 0;
     for (int r = 0; r < d.role_count; ++r) maxP = std::max(maxP, d.policy_dist_count[r]);
     const int npos = d.input_columns * d.input_rows;
-    net->smem = 2 * act_bytes + scratch_bytes(npos, d.input_channels, net->K0, d.role_count, maxP,
-                                              d.value_hidden_size);
+    // LDS: two ping-pong activation images per board; the scratch (input staging, heads) aliases
+    // the second image set, which holds nothing live at those times.
+    const int scr = scratch_bytes(npos, d.input_channels, net->K0, d.role_count, maxP, d.value_hidden_size);
+    net->smem = kc.nb * kc.act_bytes + std::max(kc.nb * kc.act_bytes, scr);
     KParams& kp = net->kp;
     kp.C = d.input_channels;
     kp.K0 = net->K0;
@@ -325,8 +365,9 @@ static int launch(gz_net* net, hipStream_t stream, const float* d_planes, int n,
     KParams kp = net->kp;
     for (int r = 0; r < kp.R; ++r) kp.pol[r] = d_pol[r];
     kp.val = d_val;
+    kp.n = n;
     void* args[] = {&kp, &d_planes};
-    HIPCHK(hipLaunchKernel(net->kfn, dim3(n), dim3(kThreads), args, net->smem, stream));
+    HIPCHK(hipLaunchKernel(net->kfn, dim3((n + net->nb - 1) / net->nb), dim3(256), args, net->smem, stream));
     return 0;
 }
 
