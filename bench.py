@@ -2,13 +2,15 @@
 (BASELINE.json configs[1]: 6-block x 128-filter net, eval batch 256), on N GPUs of one node.
 
 One process per GPU (torchrun for N>1).  Each rank runs the native self-play runner on its GPU:
-T host threads x P game pools x 256 games, one HIP stream per pool, the fused HIP forward per
-batch.  Games shard across ranks by global game index (no data-path collective); RCCL is used only
-to broadcast the weight blob from rank 0 (the generation-roll hook) before timing.
+T engine threads x P game pools x 256 games (eval batch 256 per pool, as the reference's
+Supervisor batch_size); one launcher thread merges the pools waiting for predictions into
+segmented launches of the fused HIP forward.  Games shard across ranks by global game index (no
+data-path collective); RCCL is used only to broadcast the weight blob from rank 0 (the
+generation-roll hook) before timing.
 
-A "step" = one NN batch (256 leaf evaluations) on every pool of every rank.  W warmup steps, then
-exactly K timed steps bracketed by barrier + synchronize; the time is the max over ranks, `value` is
-whole-job leaf-evals/sec.  Rank 0 prints one JSON line.
+A "step" = one eval batch (256 leaf evaluations) for every pool of the rank, i.e. T*P*256 leaf
+evaluations.  W warmup steps, then exactly K timed steps bracketed by barrier + synchronize; the
+time is the max over ranks, `value` is whole-job leaf-evals/sec.  Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -25,8 +27,8 @@ PEAK_BF16_TFLOPS = 2500.0      # gfx950 dense bf16 MFMA (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1500)
-    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--threads", type=int, default=0, help="host threads per GPU (0: auto)")
     ap.add_argument("--pools", type=int, default=2, help="game pools per thread")
     ap.add_argument("--batch", type=int, default=256)
@@ -35,6 +37,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--spin-yield", type=int, default=1000,
+                    help="yield a game's coroutine after this many NN-free playouts (0: reference behaviour)")
     return ap.parse_args()
 
 
@@ -133,10 +137,11 @@ def main():
     net.set_weights_device(blob.data_ptr(), net.weight_count)
 
     cpus = os.cpu_count() or 4
-    threads = args.threads or max(1, min(15, cpus // max(1, world) - 1))
+    threads = args.threads or max(1, min(14, cpus // max(1, world) - 2))   # + launcher + main
     runner = SelfPlayRunner(net, sm, transformer, selfplay_conf(args.mode, args.evals), device=local_rank,
                             num_threads=threads, pools_per_thread=args.pools, batch_size=args.batch,
-                            seed=args.seed, game_index_base=rank * threads * args.pools * args.batch)
+                            seed=args.seed, game_index_base=rank * threads * args.pools * args.batch,
+                            spin_yield_playouts=args.spin_yield)
     npools = runner.num_pools
 
     def barrier():
@@ -144,12 +149,21 @@ def main():
         if world > 1:
             dist.barrier()
 
+    rows_per_step = npools * args.batch
+    t_start = time.perf_counter()
+
+    def heartbeat(st):
+        el = time.perf_counter() - t_start
+        print("[bench rank %d] %.0fs rows %d (%.0f/s) launches %d games %d" %
+              (rank, el, st["rows"], st["rows"] / max(el, 1e-9), st["kernel_launches"], st["games_completed"]),
+              file=sys.stderr, flush=True)
+
     runner.start()
-    runner.wait_batches(args.warmup * npools, timeout_s=3600)
+    runner.wait_rows(args.warmup * rows_per_step, timeout_s=3600, progress=heartbeat)
     barrier()
     s0 = runner.stats()
     t0 = time.perf_counter()
-    runner.wait_batches((args.warmup + args.steps) * npools, timeout_s=3600)
+    runner.wait_rows((args.warmup + args.steps) * rows_per_step, timeout_s=3600, progress=heartbeat)
     s1 = runner.stats()
     t1 = time.perf_counter()
     barrier()
@@ -159,12 +173,12 @@ def main():
 
     d = {k: s1[k] - s0[k] for k in s1}
     vec = torch.tensor([d["rows"], d["batches"], d["games_completed"], d["games_with_samples"], d["samples"],
-                        d["kernel_ms"], d["kernel_launches"], elapsed], dtype=torch.float64, device="cuda")
+                        d["kernel_ms"], d["kernel_launches"], d["segments"]], dtype=torch.float64, device="cuda")
     tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(vec, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    rows, batches, games, games_s, samples, kms, launches, _ = vec.tolist()
+    rows, batches, games, games_s, samples, kms, launches, segments = vec.tolist()
     T = tmax.item()
 
     if rank == 0:
@@ -195,7 +209,8 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_BF16_TFLOPS, "traffic": None,
                          "kernel": "gznn::forward_kernel<128,8,8>", "avg_kernel_ms": avg_kernel_s * 1e3,
-                         "rows_per_launch": rows_per_launch, "flop_per_leaf": flops},
+                         "rows_per_launch": rows_per_launch, "pools_per_launch": segments / launches if launches else None,
+                         "flop_per_leaf": flops, "aggregate_tflops": flops * rows / T / 1e12},
             "gpu_busy_frac": (kms / 1e3) / (T * world) if T > 0 else None,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -73,6 +73,7 @@ def nn_lib():
                                               ctypes.c_void_p]
         lib.gz_net_last_kernel_ms.restype = ctypes.c_float
         lib.gz_net_last_kernel_ms.argtypes = [ctypes.c_void_p]
+        lib.gz_net_stamp_avg.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
         lib.gz_net_flops_per_eval.restype = ctypes.c_double
         lib.gz_net_flops_per_eval.argtypes = [ctypes.c_void_p]
         lib.gz_nn_last_error.restype = ctypes.c_char_p
@@ -150,6 +151,11 @@ class HipNet(object):
     def last_kernel_ms(self):
         return self.lib.gz_net_last_kernel_ms(self.handle)
 
+    def stamp_avg(self):
+        out = (ctypes.c_double * 8)()
+        self.lib.gz_net_stamp_avg(self.handle, out)
+        return list(out)
+
     def flops_per_eval(self):
         return self.lib.gz_net_flops_per_eval(self.handle)
 
@@ -192,7 +198,7 @@ class GzPuctConfig(ctypes.Structure):
                 ("use_legals_count_draw", ctypes.c_int),
                 ("backup_finalised", ctypes.c_int),
                 ("lookup_transpositions", ctypes.c_int),
-                ("evaluation_multiplier_to_convergence", ctypes.c_float)]
+                ("evaluation_multiplier_to_convergence", ctypes.c_float), ("spin_yield_playouts", ctypes.c_int)]
 
 
 class GzSelfPlayConfig(ctypes.Structure):
@@ -282,6 +288,7 @@ _ENGINE_SIGS = {
     "gz_pool_poll": (ctypes.c_int, [_VP, ctypes.c_int]),
     "gz_pool_get_stats": (ctypes.c_int, [_VP, ctypes.POINTER(GzPoolStats)]),
     "gz_pool_fetch_samples": (_VP, [_VP]),
+    "gz_pool_fetch_samples_n": (_VP, [_VP, ctypes.POINTER(ctypes.c_long)]),
     "gz_pool_take_sample_count": (ctypes.c_long, [_VP]),
 }
 
@@ -326,7 +333,7 @@ def make_puct_config(conf):
     d = confs.PUCTEvaluatorConfig()
     c = GzPuctConfig()
     for name, ctype in GzPuctConfig._fields_:
-        v = _get(conf, name, getattr(d, name))
+        v = _get(conf, name, getattr(d, name, 0))
         if name == "choose":
             if isinstance(v, str):
                 v = _CHOOSE.get(v, 0)
@@ -356,14 +363,16 @@ def make_selfplay_config(conf):
 class GzRunnerConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("num_threads", ctypes.c_int), ("pools_per_thread", ctypes.c_int),
                 ("batch_size", ctypes.c_int), ("seed", ctypes.c_ulonglong), ("game_index_base", ctypes.c_long),
-                ("per_pool_unique_states", ctypes.c_int)]
+                ("per_pool_unique_states", ctypes.c_int), ("keep_samples", ctypes.c_int),
+                ("max_launch_rows", ctypes.c_int)]
 
 
 class GzRunnerStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_long), ("rows", ctypes.c_long), ("kernel_ms", ctypes.c_double),
                 ("kernel_launches", ctypes.c_long), ("games_completed", ctypes.c_long),
                 ("games_with_samples", ctypes.c_long), ("samples", ctypes.c_long), ("no_samples", ctypes.c_long),
-                ("resigns", ctypes.c_long), ("aborts", ctypes.c_long), ("dupes", ctypes.c_long)]
+                ("resigns", ctypes.c_long), ("aborts", ctypes.c_long), ("dupes", ctypes.c_long),
+                ("segments", ctypes.c_long)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -377,6 +386,9 @@ def runner_lib():
                                          ctypes.POINTER(GzSelfPlayConfig), _IP, ctypes.c_int, ctypes.c_int]
         lib.gz_runner_start.argtypes = [_VP]
         lib.gz_runner_wait_batches.argtypes = [_VP, ctypes.c_long, ctypes.c_double]
+        lib.gz_runner_wait_rows.argtypes = [_VP, ctypes.c_long, ctypes.c_double]
+        lib.gz_runner_fetch_samples.restype = _VP
+        lib.gz_runner_fetch_samples.argtypes = [_VP]
         lib.gz_runner_stats_get.argtypes = [_VP, ctypes.POINTER(GzRunnerStats)]
         lib.gz_runner_stop.argtypes = [_VP]
         lib.gz_runner_destroy.argtypes = [_VP]

@@ -72,6 +72,7 @@ static PuctConfig to_puct(const gz_puct_config& c) {
     p.backup_finalised = c.backup_finalised != 0;
     p.lookup_transpositions = c.lookup_transpositions != 0;
     p.evaluation_multiplier_to_convergence = c.evaluation_multiplier_to_convergence;
+    p.spin_yield_playouts = c.spin_yield_playouts;
     return p;
 }
 
@@ -471,6 +472,15 @@ extern "C" int gz_pool_get_stats(gz_pool* p, gz_pool_stats* out) {
 }
 extern "C" char* gz_pool_fetch_samples(gz_pool* p) {
     std::vector<Sample*>& s = p->impl->getSamples();
+    if (s.empty()) return nullptr;
+    std::string j = samples_json(s, p->num_bases);
+    for (Sample* x : s) delete x;
+    s.clear();
+    return dup_string(j);
+}
+extern "C" char* gz_pool_fetch_samples_n(gz_pool* p, long* count) {
+    std::vector<Sample*>& s = p->impl->getSamples();
+    *count = (long)s.size();
     if (s.empty()) return nullptr;
     std::string j = samples_json(s, p->num_bases);
     for (Sample* x : s) delete x;

@@ -33,6 +33,13 @@ struct PuctConfig {
     bool backup_finalised = false;
     bool lookup_transpositions = false;
     float evaluation_multiplier_to_convergence = 1.0f;
+    // Build extension (not in the reference config, default off = reference behaviour): after this
+    // many consecutive tree playouts without a new NN evaluation, playoutMain yields to the
+    // scheduler, as the reference's playoutWorker already does for its tight loop
+    // (evaluator.cpp:725-730).  A game stuck proving a lost root (every playout ends on a terminal
+    // node, evaluator.cpp:794-841 has no break for it) then no longer stalls its pool mates; the
+    // game's own search is unchanged (batch-invariant NN, per-game RNG).
+    int spin_yield_playouts = 0;
 };
 
 struct SelfPlayConfig {

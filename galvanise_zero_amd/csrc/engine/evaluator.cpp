@@ -689,6 +689,7 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
     const int max_tree_playouts = 4 * max_non_converged_evaluations;
 
     Path path;
+    int evals_seen = stats.num_evaluations, quiet_playouts = 0;   // spin_yield_playouts (config.h)
     while (true) {
         const int our_role_index = root->lead_role_index;
         const bool is_converged = converged(conf->converged_visits);
@@ -714,6 +715,16 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
         const int depth = treePlayout(root, path);
         stats.playouts_max_depth = std::max(depth, stats.playouts_max_depth);
         stats.playouts_total_depth += depth;
+
+        if (conf->spin_yield_playouts > 0) {
+            if (stats.num_evaluations != evals_seen) {
+                evals_seen = stats.num_evaluations;
+                quiet_playouts = 0;
+            } else if (++quiet_playouts >= conf->spin_yield_playouts) {
+                quiet_playouts = 0;
+                scheduler->yield();
+            }
+        }
     }
 }
 

@@ -22,6 +22,16 @@
 namespace gznn {
 
 constexpr int kMaxRoles = 4;
+constexpr int kMaxSegments = 32;
+
+// One contiguous run of boards of a launch: its planes and outputs may live anywhere the device
+// can address (HBM, or pinned host memory of a game pool: zero-copy gather / scatter).
+struct Segment {
+    int row0;                      // first board of the segment within the launch
+    const float* planes;           // [rows][C][H][W]
+    float* pol[kMaxRoles];         // [rows][P_r]
+    float* val;                    // [rows][V]
+};
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -33,15 +43,16 @@ struct KParams {
     const float* bres;       // [2B][F]
     const float* wh;         // head 1x1 convs (BN folded) [2R+1][F]
     const float* bh;         // [2R+1]
-    const float* pd[kMaxRoles];   // policy dense [2HW][P_r]
+    const float* pd[kMaxRoles];   // policy dense, transposed [P_r][2HW]
     const float* pb[kMaxRoles];   // [P_r]
-    const float* vhw;        // value hidden [HW][VH]
+    const float* vhw;        // value hidden, transposed [VH][HW]
     const float* vhb;        // [VH]
     const float* vdw;        // value dense [VH][V]
     const float* vdb;        // [V]
-    float* pol[kMaxRoles];   // outputs [n][P_r]
-    float* val;              // outputs [n][V]
     int n;                   // boards in this launch
+    int nseg;                // segments (>= 1), ascending row0, seg[0].row0 == 0
+    Segment seg[kMaxSegments];
+    unsigned long long* stamps;   // diagnostics only (GZ_KERNEL_STAMPS): [grid][8] s_memtime per phase
     int C, K0, B, R, VH, V, leaky, flatten_nchw, maxP;
     int P[kMaxRoles];
 };
@@ -117,6 +128,63 @@ __device__ __forceinline__ float block_reduce(float v, float* red) {
     return r;
 }
 
+__device__ __forceinline__ int find_segment(const KParams& kp, int board) {
+    int s = 0;
+    while (s + 1 < kp.nseg && board >= kp.seg[s + 1].row0) ++s;
+    return s;
+}
+
+// out[j] = bias[j] + sum_i WT[j][i] * x[i] for j < rows (x in LDS, WT row-major in global, fp32):
+// 16 lanes per output row, 4 rows per wave, so every load instruction reads four 64-byte runs and
+// each row's partial sums meet in a 4-step shuffle.  U row groups are in flight per wave at once:
+// the loads of a group are independent, and issuing U*K/16 of them back to back turns U L2 round
+// trips into one.
+template <int K, int NWAVES>
+__device__ __forceinline__ void dense_rows(const float* __restrict__ WT, const float* __restrict__ bias, int rows,
+                                           const float* __restrict__ x, float* __restrict__ out, int wave, int lane) {
+    constexpr int U = K <= 64 ? 8 : 4;
+    constexpr int NI = (K + 15) / 16;
+    const int l16 = lane & 15, sub = lane >> 4;
+    float xv[NI];
+#pragma unroll
+    for (int n = 0; n < NI; ++n) xv[n] = (l16 + 16 * n < K) ? x[l16 + 16 * n] : 0.f;
+    for (int j0 = 4 * wave + sub; j0 < rows; j0 += 4 * NWAVES * U) {
+        float s[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + u * 4 * NWAVES;
+            const float* wr = WT + (size_t)(j < rows ? j : 0) * K;
+            s[u] = 0.f;
+#pragma unroll
+            for (int n = 0; n < NI; ++n)
+                if (l16 + 16 * n < K) s[u] += wr[l16 + 16 * n] * xv[n];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float v = s[u];
+            v += __shfl_xor(v, 8, 64);
+            v += __shfl_xor(v, 4, 64);
+            v += __shfl_xor(v, 2, 64);
+            v += __shfl_xor(v, 1, 64);
+            const int j = j0 + u * 4 * NWAVES;
+            if (l16 == 0 && j < rows) out[j] = v + bias[j];
+        }
+    }
+}
+
+// Weight prefetch that the compiler cannot move: issued as inline asm at the top of an iteration
+// and consumed after an explicit vmcnt(0) at its end.  (Plain loads get sunk past the loop back
+// edge to right before their first MFMA, which exposes the whole L2 latency every iteration.)
+// The compiler does not track these loads, so gload_wait_all must precede any use of the result;
+// gload_ready then re-defines each register after the wait so no copy can be hoisted above it.
+__device__ __forceinline__ bf16x8 gload_issue(const __bf16* p) {
+    bf16x8 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void gload_wait_all(bf16x8& v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)::"memory"); }
+__device__ __forceinline__ void gload_ready(bf16x8& v) { asm volatile("" : "+v"(v)); }
+
 // One 3x3 'same' conv over the NB LDS images at X (board b at X + b*ACT_BYTES):
 // acc[ct][t] = W * X (fp32 accumulate), tile t = b*PT + pt.  Every weight fragment loaded from L2
 // feeds TT = NB*PT MFMAs -- NB is the weight-reuse factor that sets the L2->CU byte rate.
@@ -126,10 +194,13 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, const __bf16
                                         int co_base, int li, int g) {
     using G = Geo<F, H, W, NB>;
     constexpr int CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC;
-    // weight prefetch depth in k-steps; D | KC keeps the ring index a compile-time constant while
-    // the tap loop stays rolled (a rolled tap loop keeps the LDS address math out of registers)
-    constexpr int D = KC < 4 ? KC : 4;
-    static_assert(KC % D == 0, "prefetch depth must divide the k-steps per tap");
+    // The k loop runs as 9*KC/KS rolled iterations of KS k-steps (KS | KC, a tap or part of one).
+    // Each iteration first issues the weight fragments of the NEXT iteration (one full iteration
+    // of MFMAs hides their L2 latency), and double-buffers the activation fragments from LDS one
+    // k-step ahead.  A rolled loop keeps the LDS address math out of registers.
+    constexpr int KS = KC < 4 ? KC : 4;
+    constexpr int NIT = 9 * KC / KS;
+    static_assert(KC % KS == 0, "k-steps per iteration must divide the k-steps per tap");
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
@@ -137,15 +208,30 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, const __bf16
 
     // lane's fragment of step s = tap*KC + kc: wp + ((s*F + co_base + 16ct + li) * 32 + 8g)
     const __bf16* wl = wp + (size_t)(co_base + li) * 32 + 8 * g;
-    bf16x8 ring[D][CT];
+    bf16x8 cur[KS][CT];
 #pragma unroll
-    for (int d = 0; d < D; ++d)
+    for (int k = 0; k < KS; ++k)
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
-            ring[d][ct] = *(const bf16x8*)(wl + ((size_t)d * F + 16 * ct) * 32);
+            cur[k][ct] = *(const bf16x8*)(wl + ((size_t)k * F + 16 * ct) * 32);
+    // land the first fragments before the loop so the loop header carries no pending loads
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) gload_ready(cur[k][ct]);
 
 #pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
+    for (int it = 0; it < NIT; ++it) {
+        const int itn = it + 1 < NIT ? it + 1 : it;     // the last iteration re-reads its own
+        bf16x8 nxt[KS][CT];
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+                nxt[k][ct] = gload_issue(wl + ((size_t)(itn * KS + k) * F + 16 * ct) * 32);
+
+        const int s0 = it * KS;
+        const int tap = s0 / KC, kc0 = s0 % KC;
         const int dy = tap / 3 - 1, dx = tap % 3 - 1;
         int qoff[PT], qswz[PT];
 #pragma unroll
@@ -157,27 +243,34 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, const __bf16
             qoff[pt] = q * G::ROWB;
             qswz[pt] = q & G::SWZ;
         }
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-            bf16x8 b[TT];
+        bf16x8 b[2][TT];
+        auto load_b = [&](int kc, bf16x8 (&dst)[TT]) {
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) {
                 const int off = qoff[pt] + (((kc * 4 + g) ^ qswz[pt]) << 4);
 #pragma unroll
-                for (int bb = 0; bb < NB; ++bb) b[bb * PT + pt] = *(const bf16x8*)(X + bb * G::ACT_BYTES + off);
+                for (int bb = 0; bb < NB; ++bb) dst[bb * PT + pt] = *(const bf16x8*)(X + bb * G::ACT_BYTES + off);
             }
+        };
+        load_b(kc0, b[0]);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            if (k + 1 < KS) load_b(kc0 + k + 1, b[(k + 1) & 1]);
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
                 for (int t = 0; t < TT; ++t)
-                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[kc % D][ct], b[t], acc[ct][t], 0, 0, 0);
-            // prefetch step s + D (clamped to the last step: the tail re-reads it harmlessly)
-            int sn = tap * KC + kc + D;
-            sn = sn < 9 * KC ? sn : 9 * KC - 1;
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct)
-                ring[kc % D][ct] = *(const bf16x8*)(wl + ((size_t)sn * F + 16 * ct) * 32);
+                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[k][ct], b[k & 1][t], acc[ct][t], 0, 0, 0);
         }
+        // the prefetched fragments have had a whole iteration to land
+        gload_wait_all(nxt[0][0]);
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                gload_ready(nxt[k][ct]);
+                cur[k][ct] = nxt[k][ct];
+            }
     }
 }
 
@@ -185,7 +278,7 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, const __bf16
 // allocation must allow (amdgpu_waves_per_eu), i.e. WPE workgroups per CU.
 template <int F, int H, int W, int NB, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
-forward_kernel(KParams kp, const float* __restrict__ planes) {
+forward_kernel(const KParams kp) {
     using G = Geo<F, H, W, NB>;
     constexpr int NPOS = G::NPOS, PT = G::PT, TT = G::TT, CT = G::CT, kThreads = 256;
     constexpr int ACT = G::ACT_BYTES;
@@ -197,6 +290,9 @@ forward_kernel(KParams kp, const float* __restrict__ planes) {
 
     const int board0 = blockIdx.x * NB;
     const int tid = threadIdx.x;
+#define GZ_STAMP(i) \
+    if (kp.stamps && tid == 0) kp.stamps[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime()
+    GZ_STAMP(0);
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, li = lane & 15;
@@ -219,19 +315,24 @@ forward_kernel(KParams kp, const float* __restrict__ planes) {
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
         const bool live = board0 + bb < kp.n;
-        const float* in = planes + (size_t)(board0 + bb) * C * NPOS;
+        const int sg = find_segment(kp, board0 + bb);
+        const float* in = kp.seg[sg].planes + (size_t)(board0 + bb - kp.seg[sg].row0) * C * NPOS;
         for (int i = tid; i < C * NPOS; i += kThreads) sin[i] = live ? in[i] : 0.f;
         __syncthreads();
-        // IM[p][k], k = tap*C + c, zero padded to K0
-        for (int i = tid; i < (NPOS + 1) * K0; i += kThreads) {
-            const int p = i / K0, k = i - (i / K0) * K0;
-            float v = 0.f;
-            if (p < NPOS && k < 9 * C) {
-                const int tap = k / C, c = k - (k / C) * C;
-                const int y = p / W + tap / 3 - 1, x = p % W + tap % 3 - 1;
-                if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) v = sin[c * NPOS + y * W + x];
+        // IM[p][k], k = tap*C + c, zero padded to K0: zero the image, then one thread per
+        // (position, tap) copies its C channels (compile-time divisors only)
+        for (int i = tid; i < (NPOS + 1) * K0 / 8; i += kThreads) ((uint4*)IM)[i] = uint4{0u, 0u, 0u, 0u};
+        __syncthreads();
+        for (int i = tid; i < NPOS * 9; i += kThreads) {
+            const int p = i / 9, tap = i - (i / 9) * 9;
+            const int y = p / W + tap / 3 - 1, x = p % W + tap % 3 - 1;
+            if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
+                const float* src = sin + y * W + x;
+                for (int c = 0; c < C; ++c) {
+                    const int k = tap * C + c;
+                    *(__bf16*)(IM + p * imrow + ((((k >> 3) ^ (p & imswz))) << 4) + (k & 7) * 2) = (__bf16)src[c * NPOS];
+                }
             }
-            *(__bf16*)(IM + p * imrow + ((((k >> 3) ^ (p & imswz))) << 4) + (k & 7) * 2) = (__bf16)v;
         }
         __syncthreads();
 
@@ -278,6 +379,7 @@ forward_kernel(KParams kp, const float* __restrict__ planes) {
     }
     __syncthreads();
 
+    GZ_STAMP(1);
     // ---- residual tower ------------------------------------------------------------------
     constexpr size_t conv_elems = (size_t)9 * F * F;
     for (int blk = 0; blk < kp.B; ++blk) {
@@ -323,6 +425,7 @@ forward_kernel(KParams kp, const float* __restrict__ planes) {
         __syncthreads();
     }
 
+    GZ_STAMP(2);
     // ---- heads, one board at a time: 1x1 convs (2 per policy role + 1 value) from the fp32
     // residual registers, then the dense layers + softmaxes in fp32 -------------------------
     const int HC = 2 * kp.R + 1;
@@ -334,6 +437,8 @@ forward_kernel(KParams kp, const float* __restrict__ planes) {
     for (int bb = 0; bb < NB; ++bb) {
         const int board = board0 + bb;
         const bool live = board < kp.n;
+        const int sg = find_segment(kp, board);
+        const int row = board - kp.seg[sg].row0;
         for (int h = 0; h < HC; ++h) {
             float wv[CT][4];
 #pragma unroll
@@ -370,19 +475,17 @@ forward_kernel(KParams kp, const float* __restrict__ planes) {
             }
         }
         __syncthreads();
+        if (bb == 0) GZ_STAMP(3);
 
         // policy heads: Dense(2HW -> P_r) + softmax
         for (int r = 0; r < kp.R; ++r) {
             const int P = kp.P[r];
             const float* pf = feat + r * 2 * NPOS;
             const float* wd = kp.pd[r];
+            dense_rows<2 * NPOS, 4>(wd, kp.pb[r], P, pf, lg, wave, lane);
+            __syncthreads();
             float lmax = -3.0e38f;
-            for (int j = tid; j < P; j += kThreads) {
-                float z = kp.pb[r][j];
-                for (int i = 0; i < 2 * NPOS; ++i) z += pf[i] * wd[(size_t)i * P + j];
-                lg[j] = z;
-                lmax = fmaxf(lmax, z);
-            }
+            for (int j = tid; j < P; j += kThreads) lmax = fmaxf(lmax, lg[j]);
             const float m = block_reduce<true, 4>(lmax, red);
             float lsum = 0.f;
             for (int j = tid; j < P; j += kThreads) {
@@ -393,19 +496,18 @@ forward_kernel(KParams kp, const float* __restrict__ planes) {
             const float ssum = block_reduce<false, 4>(lsum, red);
             const float inv = 1.f / ssum;
             if (live) {
-                float* out = kp.pol[r] + (size_t)board * P;
+                float* out = kp.seg[sg].pol[r] + (size_t)row * P;
                 for (int j = tid; j < P; j += kThreads) out[j] = lg[j] * inv;
             }
             __syncthreads();
         }
 
+        if (bb == 0) GZ_STAMP(4);
         // value head: Dense(HW -> VH) + act, Dense(VH -> V) + softmax
         const float* vf = feat + 2 * kp.R * NPOS;
-        for (int k = tid; k < kp.VH; k += kThreads) {
-            float z = kp.vhb[k];
-            for (int p = 0; p < NPOS; ++p) z += vf[p] * kp.vhw[(size_t)p * kp.VH + k];
-            lg[k] = act_fn(z, kp.leaky);
-        }
+        dense_rows<NPOS, 4>(kp.vhw, kp.vhb, kp.VH, vf, lg, wave, lane);
+        __syncthreads();
+        for (int k = tid; k < kp.VH; k += kThreads) lg[k] = act_fn(lg[k], kp.leaky);
         __syncthreads();
         if (wave < kp.V) {
             float s = 0.f;
@@ -419,10 +521,12 @@ forward_kernel(KParams kp, const float* __restrict__ planes) {
             for (int v = 1; v < kp.V; ++v) m = fmaxf(m, red[16 + v]);
             float e[4], sum = 0.f;
             for (int v = 0; v < kp.V; ++v) { e[v] = __expf(red[16 + v] - m); sum += e[v]; }
-            for (int v = 0; v < kp.V; ++v) kp.val[(size_t)board * kp.V + v] = e[v] / sum;
+            for (int v = 0; v < kp.V; ++v) kp.seg[sg].val[(size_t)row * kp.V + v] = e[v] / sum;
         }
         __syncthreads();    // scratch is reused by the next board
     }
+    GZ_STAMP(5);
+#undef GZ_STAMP
 }
 
 }  // namespace gznn

@@ -30,7 +30,6 @@ static int fail(const std::string& msg) {
         if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-typedef void (*kernel_fn)(KParams, const float*);
 
 struct gz_net {
     gz_net_desc d;
@@ -50,6 +49,10 @@ struct gz_net {
     float* d_io = nullptr;         // staging: planes + outputs
     int io_cap = 0;
     float last_ms = 0.f;
+    unsigned long long* d_stamps = nullptr;   // GZ_KERNEL_STAMPS diagnostics
+    int stamp_cap = 0;
+    bool stamps_on = false;
+    double stamp_avg[8] = {0};
 };
 
 extern "C" const char* gz_nn_last_error(void) { return g_err.c_str(); }
@@ -187,6 +190,7 @@ extern "C" void gz_net_destroy(gz_net* net) {
     (void)hipSetDevice(net->device);
     if (net->dmem) (void)hipFree(net->dmem);
     if (net->d_io) (void)hipFree(net->d_io);
+    if (net->d_stamps) (void)hipFree(net->d_stamps);
     if (net->ev0) (void)hipEventDestroy(net->ev0);
     if (net->ev1) (void)hipEventDestroy(net->ev1);
     if (net->stream) (void)hipStreamDestroy(net->stream);
@@ -317,10 +321,21 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     put(o_wh, wh.data(), wh.size() * 4);
     put(o_bh, bh.data(), bh.size() * 4);
     for (int r = 0; r < R; ++r) {
-        put(o_pd[r], pdense[r], (size_t)2 * HW * d.policy_dist_count[r] * 4);
+        // transposed to [P_r][2HW]: one output row is contiguous for the row-parallel dense
+        const int P = d.policy_dist_count[r];
+        std::vector<float> t((size_t)P * 2 * HW);
+        for (int i = 0; i < 2 * HW; ++i)
+            for (int j = 0; j < P; ++j) t[(size_t)j * 2 * HW + i] = pdense[r][(size_t)i * P + j];
+        put(o_pd[r], t.data(), t.size() * 4);
         put(o_pb[r], pbias[r], (size_t)d.policy_dist_count[r] * 4);
     }
-    put(o_vhw, vhw, (size_t)HW * d.value_hidden_size * 4);
+    {   // transposed to [VH][HW]
+        const int VH = d.value_hidden_size;
+        std::vector<float> t((size_t)VH * HW);
+        for (int p = 0; p < HW; ++p)
+            for (int k = 0; k < VH; ++k) t[(size_t)k * HW + p] = vhw[(size_t)p * VH + k];
+        put(o_vhw, t.data(), t.size() * 4);
+    }
     put(o_vhb, vhb, d.value_hidden_size * 4);
     put(o_vdw, vdw, (size_t)d.value_hidden_size * d.num_values * 4);
     put(o_vdb, vdb, d.num_values * 4);
@@ -358,23 +373,49 @@ extern "C" int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_
     return gz_net_set_weights(net, h.data(), count);
 }
 
-static int launch(gz_net* net, hipStream_t stream, const float* d_planes, int n,
-                  float* const* d_pol, float* d_val) {
+static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* segs, int nseg) {
     if (!net->has_weights) return fail("weights not set");
-    if (n <= 0) return 0;
+    if (nseg < 1 || nseg > kMaxSegments) return fail("segment count out of range (1.." + std::to_string(kMaxSegments) + ")");
     KParams kp = net->kp;
-    for (int r = 0; r < kp.R; ++r) kp.pol[r] = d_pol[r];
-    kp.val = d_val;
+    int n = 0;
+    for (int i = 0; i < nseg; ++i) {
+        if (segs[i].rows < 0) return fail("negative segment rows");
+        Segment& g = kp.seg[i];
+        g.row0 = n;
+        g.planes = segs[i].planes;
+        for (int r = 0; r < kp.R; ++r) g.pol[r] = segs[i].policies[r];
+        g.val = segs[i].values;
+        n += segs[i].rows;
+    }
+    if (n <= 0) return 0;
     kp.n = n;
-    void* args[] = {&kp, &d_planes};
+    kp.nseg = nseg;
+    kp.stamps = net->stamps_on ? net->d_stamps : nullptr;
+    void* args[] = {&kp};
     HIPCHK(hipLaunchKernel(net->kfn, dim3((n + net->nb - 1) / net->nb), dim3(256), args, net->smem, stream));
     return 0;
+}
+
+static int launch(gz_net* net, hipStream_t stream, const float* d_planes, int n,
+                  float* const* d_pol, float* d_val) {
+    if (n <= 0) return net->has_weights ? 0 : fail("weights not set");
+    gz_segment sg{};
+    sg.rows = n;
+    sg.planes = d_planes;
+    for (int r = 0; r < net->kp.R; ++r) sg.policies[r] = d_pol[r];
+    sg.values = d_val;
+    return launch_segments(net, stream, &sg, 1);
 }
 
 extern "C" int gz_net_forward_device(gz_net* net, void* stream, const float* d_planes, int n,
                                      float* const* d_policies, float* d_values) {
     if (!net) return fail("null net");
     return launch(net, (hipStream_t)stream, d_planes, n, d_policies, d_values);
+}
+
+extern "C" int gz_net_forward_segments(gz_net* net, void* stream, const gz_segment* segs, int nseg) {
+    if (!net || !segs) return fail("null argument");
+    return launch_segments(net, (hipStream_t)stream, segs, nseg);
 }
 
 extern "C" int gz_net_forward(gz_net* net, const float* planes, int n, float* const* policies, float* values) {
@@ -397,14 +438,36 @@ extern "C" int gz_net_forward(gz_net* net, const float* planes, int n, float* co
     for (int r = 0; r < d.role_count; ++r) { d_pol[r] = p; p += (size_t)n * d.policy_dist_count[r]; }
     float* d_val = p;
     HIPCHK(hipMemcpyAsync(d_in, planes, (size_t)n * in_f * 4, hipMemcpyHostToDevice, net->stream));
+    const bool stamps = getenv("GZ_KERNEL_STAMPS") != nullptr;
+    const int grid = (n + net->nb - 1) / net->nb;
+    if (stamps && grid > net->stamp_cap) {
+        if (net->d_stamps) HIPCHK(hipFree(net->d_stamps));
+        HIPCHK(hipMalloc((void**)&net->d_stamps, (size_t)grid * 8 * sizeof(unsigned long long)));
+        net->stamp_cap = grid;
+    }
     HIPCHK(hipEventRecord(net->ev0, net->stream));
-    if (launch(net, net->stream, d_in, n, d_pol, d_val)) return -1;
+    net->stamps_on = stamps;
+    const int lrc = launch(net, net->stream, d_in, n, d_pol, d_val);
+    net->stamps_on = false;
+    if (lrc) return -1;
     HIPCHK(hipEventRecord(net->ev1, net->stream));
     for (int r = 0; r < d.role_count; ++r)
         HIPCHK(hipMemcpyAsync(policies[r], d_pol[r], (size_t)n * d.policy_dist_count[r] * 4, hipMemcpyDeviceToHost, net->stream));
     HIPCHK(hipMemcpyAsync(values, d_val, (size_t)n * d.num_values * 4, hipMemcpyDeviceToHost, net->stream));
     HIPCHK(hipStreamSynchronize(net->stream));
     HIPCHK(hipEventElapsedTime(&net->last_ms, net->ev0, net->ev1));
+    if (stamps) {
+        std::vector<unsigned long long> h((size_t)grid * 8);
+        HIPCHK(hipMemcpy(h.data(), net->d_stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (int i = 0; i < 8; ++i) net->stamp_avg[i] = 0;
+        for (int b = 0; b < grid; ++b)
+            for (int i = 1; i < 6; ++i) net->stamp_avg[i] += (double)(h[(size_t)b * 8 + i] - h[(size_t)b * 8 + i - 1]) / grid;
+    }
+    return 0;
+}
+
+extern "C" int gz_net_stamp_avg(const gz_net* net, double* out8) {
+    for (int i = 0; i < 8; ++i) out8[i] = net->stamp_avg[i];
     return 0;
 }
 

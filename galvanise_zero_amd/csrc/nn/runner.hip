@@ -1,11 +1,15 @@
 // Native self-play driver for one GPU: the MI355X-native replacement of the reference's
 // Python poll loop (cppinterface.py:78-144) + worker threads (supervisor.cpp:79-99, 196-245).
 //
-// T host threads each own P game pools (SelfPlayManager, via the engine C-ABI).  A pool's planes
-// are written by its coroutines straight into pinned host memory; its batch is copied to HBM, run
-// through the fused forward and copied back on the pool's own HIP stream, so while the GPU
-// evaluates pool k the thread is already doing tree work for pool k+1 (the reference's
-// two-managers-per-thread ping-pong, generalised to P).  No Python per batch.
+// T engine threads each own P game pools (SelfPlayManager via the engine C-ABI).  A pool's
+// coroutines write its planes straight into the pool's pinned host buffer; the pool is then handed
+// to ONE launcher thread, which merges every pool waiting at that moment (up to GZ_MAX_SEGMENTS) into
+// a single segmented launch of the fused forward: the kernel gathers each pool's planes from host
+// memory and scatters the policies / values back into the pool's pinned output buffers, so there
+// are no staging copies and no per-pool launches.  While the GPU runs one merged batch, the next
+// accumulates (at most two batches in flight on one stream), so batch size adapts to load: under
+// GPU pressure the launches grow, which is where the kernel is most efficient.  The engine thread
+// meanwhile advances its other pools (the reference's two-managers-per-thread ping-pong, P-way).
 #include "../../../include/gzero_engine.h"
 #include "../../../include/gzero_nn.h"
 
@@ -15,30 +19,38 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
-
 static thread_local std::string g_err;
 
 namespace {
 
+enum PoolState : int { kEngine = 0, kQueued = 1, kInFlight = 2, kDead = 3 };
+
 struct Pool {
     gz_pool* pool = nullptr;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    float* h_planes = nullptr;
-    float* h_out = nullptr;          // policies then values (pinned)
-    float* d_planes = nullptr;
-    float* d_out = nullptr;
-    std::vector<float*> h_pol, d_pol;
+    float* h_planes = nullptr;       // pinned: written by the engine, read by the kernel
+    float* h_out = nullptr;          // pinned: policies then values, written by the kernel
+    std::vector<float*> h_pol;
     float* h_val = nullptr;
-    float* d_val = nullptr;
-    int rows_in_flight = 0;
+    int rows = 0;                    // rows submitted in the current launch
+    int rows_done = 0;               // rows whose predictions are in h_out (engine side)
+    std::atomic<int> state{kEngine};
 };
+
+struct Batch {
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<int> pools;
+    int rows = 0;
+};
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
 
 }  // namespace
 
@@ -52,98 +64,197 @@ struct gz_runner {
     std::vector<int> policy_sizes;
     std::vector<Pool> pools;
     std::vector<std::thread> threads;
+    std::thread launcher;
+    hipStream_t stream = nullptr;
+    Batch batches_ring[2];
+
+    std::mutex qm;                   // guards queue
+    std::condition_variable qcv;
+    std::deque<int> queue;           // pools waiting for the GPU, in submission order
+
     std::atomic<bool> stop{false};
-    std::atomic<long> batches{0}, rows{0}, launches{0}, samples_taken{0};
+    std::atomic<long> batches{0}, rows{0}, launches{0}, samples_taken{0}, segments{0};
     std::atomic<long> kernel_us{0};
     std::mutex m;
     std::condition_variable cv;
     std::atomic<int> failed{0};
     std::string fail_msg;
+    std::mutex sm_;                  // guards sample_json
+    std::string sample_json;         // comma-joined sample objects awaiting gz_runner_fetch_samples
 };
 
-#define RCHK(x)                                                                            \
-    do {                                                                                   \
-        hipError_t e_ = (x);                                                               \
-        if (e_ != hipSuccess) {                                                            \
-            g_err = std::string(#x) + ": " + hipGetErrorString(e_);                        \
-            return -1;                                                                     \
-        }                                                                                  \
-    } while (0)
-
-static int launch_pool(gz_runner* r, Pool& p, int nrows) {
-    p.rows_in_flight = nrows;
-    if (nrows == 0) return 0;
-    RCHK(hipMemcpyAsync(p.d_planes, p.h_planes, (size_t)nrows * r->total_size * 4, hipMemcpyHostToDevice, p.stream));
-    RCHK(hipEventRecord(p.ev0, p.stream));
-    if (gz_net_forward_device(r->net, p.stream, p.d_planes, nrows, p.d_pol.data(), p.d_val) != 0) {
-        g_err = gz_nn_last_error();
-        return -1;
+static void set_failed(gz_runner* r, const std::string& msg) {
+    {
+        std::lock_guard<std::mutex> lk(r->m);
+        if (!r->failed.load()) r->fail_msg = msg;
+        r->failed = 1;
     }
-    RCHK(hipEventRecord(p.ev1, p.stream));
-    for (int i = 0; i < r->num_policies; ++i)
-        RCHK(hipMemcpyAsync(p.h_pol[i], p.d_pol[i], (size_t)nrows * r->policy_sizes[i] * 4, hipMemcpyDeviceToHost,
-                            p.stream));
-    RCHK(hipMemcpyAsync(p.h_val, p.d_val, (size_t)nrows * r->num_values * 4, hipMemcpyDeviceToHost, p.stream));
-    return 0;
+    r->stop = true;
+    r->qcv.notify_all();
+    r->cv.notify_all();
 }
 
-static void thread_main(gz_runner* r, int tid) {
+// ---- engine threads ---------------------------------------------------------------------------
+static void engine_main(gz_runner* r, int tid) {
+    const int P = r->cfg.pools_per_thread;
+    std::vector<int> mine;
+    for (int k = 0; k < P; ++k) mine.push_back(tid * P + k);
+    for (int i : mine) gz_pool_start(r->pools[i].pool, &r->conf);
+    int idle = 0;
+    while (!r->stop.load(std::memory_order_relaxed)) {
+        bool progressed = false;
+        for (int i : mine) {
+            Pool& p = r->pools[i];
+            if (p.state.load(std::memory_order_acquire) != kEngine) continue;
+            const int n = gz_pool_poll(p.pool, p.rows_done);
+            if (r->cfg.keep_samples) {
+                long cnt = 0;
+                char* j = gz_pool_fetch_samples_n(p.pool, &cnt);
+                if (j) {
+                    const size_t len = std::strlen(j);   // "[{...},{...}]"
+                    std::lock_guard<std::mutex> lk(r->sm_);
+                    if (len > 2) {
+                        if (!r->sample_json.empty()) r->sample_json += ',';
+                        r->sample_json.append(j + 1, len - 2);
+                    }
+                    gz_free(j);
+                }
+                r->samples_taken.fetch_add(cnt, std::memory_order_relaxed);
+            } else {
+                r->samples_taken.fetch_add(gz_pool_take_sample_count(p.pool), std::memory_order_relaxed);
+            }
+            progressed = true;
+            if (n <= 0) {                 // main loop ended (never in self-play) or error
+                p.state.store(kDead, std::memory_order_release);
+                if (n < 0) set_failed(r, std::string("gz_pool_poll: ") + gz_engine_last_error());
+                continue;
+            }
+            p.rows = n;
+            p.state.store(kQueued, std::memory_order_release);
+            {
+                std::lock_guard<std::mutex> lk(r->qm);
+                r->queue.push_back(i);
+            }
+            r->qcv.notify_one();
+        }
+        if (progressed) {
+            idle = 0;
+        } else if (++idle < 2000) {
+            cpu_relax();
+        } else {
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+    }
+}
+
+// ---- launcher thread --------------------------------------------------------------------------
+static void launcher_main(gz_runner* r) {
     if (hipSetDevice(r->cfg.device) != hipSuccess) {
-        r->failed = 1;
+        set_failed(r, "hipSetDevice failed in launcher");
         return;
     }
-    const int P = r->cfg.pools_per_thread;
-    std::vector<Pool*> mine;
-    for (int k = 0; k < P; ++k) mine.push_back(&r->pools[(size_t)tid * P + k]);
-    // prime: start the games and produce each pool's first batch
-    for (Pool* p : mine) {
-        gz_pool_start(p->pool, &r->conf);
-        const int rows = gz_pool_poll(p->pool, 0);
-        if (launch_pool(r, *p, rows) != 0) {
-            std::lock_guard<std::mutex> lk(r->m);
-            r->fail_msg = g_err;
-            r->failed = 1;
+    const int max_rows = r->cfg.max_launch_rows > 0 ? r->cfg.max_launch_rows : 1 << 30;
+    std::deque<int> inflight;        // indices into batches_ring, oldest first
+    int next_slot = 0;
+    std::vector<gz_segment> segs;
+    while (true) {
+        // retire finished batches (in order: one stream)
+        while (!inflight.empty()) {
+            Batch& b = r->batches_ring[inflight.front()];
+            const hipError_t q = hipEventQuery(b.ev1);
+            if (q == hipErrorNotReady) break;
+            if (q != hipSuccess) {
+                set_failed(r, std::string("forward failed: ") + hipGetErrorString(q));
+                return;
+            }
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, b.ev0, b.ev1) == hipSuccess)
+                r->kernel_us.fetch_add((long)(ms * 1000.0f), std::memory_order_relaxed);
+            for (int i : b.pools) {
+                Pool& p = r->pools[i];
+                p.rows_done = p.rows;
+                p.state.store(kEngine, std::memory_order_release);
+            }
+            r->rows.fetch_add(b.rows, std::memory_order_relaxed);
+            r->batches.fetch_add(1, std::memory_order_relaxed);
+            inflight.pop_front();
+            r->cv.notify_all();
+        }
+        if (r->stop.load(std::memory_order_relaxed)) {
+            if (inflight.empty()) return;
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+            continue;
+        }
+        if (inflight.size() >= 2) {
+            cpu_relax();
+            continue;
+        }
+        // gather every waiting pool into one segmented launch
+        Batch& b = r->batches_ring[next_slot];
+        b.pools.clear();
+        b.rows = 0;
+        {
+            std::unique_lock<std::mutex> lk(r->qm);
+            if (r->queue.empty()) {
+                if (inflight.empty())
+                    r->qcv.wait_for(lk, std::chrono::microseconds(200));
+                else
+                    r->qcv.wait_for(lk, std::chrono::microseconds(5));
+            }
+            while (!r->queue.empty() && (int)b.pools.size() < GZ_MAX_SEGMENTS) {
+                const int i = r->queue.front();
+                if (!b.pools.empty() && b.rows + r->pools[i].rows > max_rows) break;
+                r->queue.pop_front();
+                b.pools.push_back(i);
+                b.rows += r->pools[i].rows;
+            }
+        }
+        if (b.pools.empty()) continue;
+        segs.assign(b.pools.size(), gz_segment{});
+        for (size_t k = 0; k < b.pools.size(); ++k) {
+            Pool& p = r->pools[b.pools[k]];
+            p.state.store(kInFlight, std::memory_order_relaxed);
+            segs[k].rows = p.rows;
+            segs[k].planes = p.h_planes;
+            for (int j = 0; j < r->num_policies; ++j) segs[k].policies[j] = p.h_pol[j];
+            segs[k].values = p.h_val;
+        }
+        if (hipEventRecord(b.ev0, r->stream) != hipSuccess ||
+            gz_net_forward_segments(r->net, r->stream, segs.data(), (int)segs.size()) != 0 ||
+            hipEventRecord(b.ev1, r->stream) != hipSuccess) {
+            set_failed(r, std::string("launch failed: ") + gz_nn_last_error());
             return;
         }
+        r->launches.fetch_add(1, std::memory_order_relaxed);
+        r->segments.fetch_add((long)segs.size(), std::memory_order_relaxed);
+        inflight.push_back(next_slot);
+        next_slot ^= 1;
     }
-    while (!r->stop.load(std::memory_order_relaxed)) {
-        for (Pool* p : mine) {
-            if (hipStreamSynchronize(p->stream) != hipSuccess) {
-                std::lock_guard<std::mutex> lk(r->m);
-                r->fail_msg = "hipStreamSynchronize failed";
-                r->failed = 1;
-                return;
-            }
-            const int done = p->rows_in_flight;
-            if (done > 0) {
-                float ms = 0.f;
-                if (hipEventElapsedTime(&ms, p->ev0, p->ev1) == hipSuccess)
-                    r->kernel_us.fetch_add((long)(ms * 1000.0f), std::memory_order_relaxed);
-                r->launches.fetch_add(1, std::memory_order_relaxed);
-                r->batches.fetch_add(1, std::memory_order_relaxed);
-                r->rows.fetch_add(done, std::memory_order_relaxed);
-            }
-            const int rows = gz_pool_poll(p->pool, done);
-            r->samples_taken.fetch_add(gz_pool_take_sample_count(p->pool), std::memory_order_relaxed);
-            if (launch_pool(r, *p, rows) != 0) {
-                std::lock_guard<std::mutex> lk(r->m);
-                r->fail_msg = g_err;
-                r->failed = 1;
-                return;
-            }
-        }
-        r->cv.notify_all();
-    }
-    for (Pool* p : mine) (void)hipStreamSynchronize(p->stream);
 }
 
 extern "C" const char* gz_runner_last_error(void) { return g_err.c_str(); }
+
+extern "C" char* gz_runner_fetch_samples(gz_runner* r) {
+    std::string out;
+    {
+        std::lock_guard<std::mutex> lk(r->sm_);
+        if (r->sample_json.empty()) return nullptr;
+        out.reserve(r->sample_json.size() + 2);
+        out += '[';
+        out += r->sample_json;
+        out += ']';
+        r->sample_json.clear();
+    }
+    char* c = (char*)std::malloc(out.size() + 1);
+    std::memcpy(c, out.c_str(), out.size() + 1);
+    return c;
+}
 
 extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_transformer* t,
                                        const gz_runner_config* cfg, const gz_selfplay_config* conf,
                                        const int* policy_sizes, int num_policies, int num_values) {
     if (!net || !sm || !t || !cfg || !conf || cfg->num_threads < 1 || cfg->pools_per_thread < 1 ||
-        cfg->batch_size < 1) {
+        cfg->batch_size < 1 || num_policies < 1 || num_policies > GZ_MAX_ROLES) {
         g_err = "bad runner arguments";
         return nullptr;
     }
@@ -161,40 +272,39 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
     r->num_policies = num_policies;
     r->num_values = num_values;
     r->policy_sizes.assign(policy_sizes, policy_sizes + num_policies);
+    bool ok = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess;
+    for (Batch& b : r->batches_ring)
+        ok = ok && hipEventCreate(&b.ev0) == hipSuccess && hipEventCreate(&b.ev1) == hipSuccess;
+    if (!ok) {
+        g_err = "stream / event creation failed";
+        gz_runner_destroy(r);
+        return nullptr;
+    }
     const int npools = cfg->num_threads * cfg->pools_per_thread;
-    r->pools.resize(npools);
+    r->pools = std::vector<Pool>(npools);
     const int B = cfg->batch_size;
     size_t out_per_row = num_values;
     for (int i = 0; i < num_policies; ++i) out_per_row += policy_sizes[i];
     for (int i = 0; i < npools; ++i) {
         Pool& p = r->pools[i];
-        bool ok = hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking) == hipSuccess &&
-                  hipEventCreate(&p.ev0) == hipSuccess && hipEventCreate(&p.ev1) == hipSuccess &&
-                  hipHostMalloc((void**)&p.h_planes, (size_t)B * r->total_size * 4, hipHostMallocDefault) == hipSuccess &&
-                  hipHostMalloc((void**)&p.h_out, (size_t)B * out_per_row * 4, hipHostMallocDefault) == hipSuccess &&
-                  hipMalloc((void**)&p.d_planes, (size_t)B * r->total_size * 4) == hipSuccess &&
-                  hipMalloc((void**)&p.d_out, (size_t)B * out_per_row * 4) == hipSuccess;
-        if (!ok) {
-            g_err = "runner allocation failed";
-            delete r;   // leaks device buffers on this error path; process is failing anyway
+        if (hipHostMalloc((void**)&p.h_planes, (size_t)B * r->total_size * 4, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&p.h_out, (size_t)B * out_per_row * 4, hipHostMallocDefault) != hipSuccess) {
+            g_err = "runner pinned allocation failed";
+            gz_runner_destroy(r);
             return nullptr;
         }
         float* ho = p.h_out;
-        float* dd = p.d_out;
         for (int k = 0; k < num_policies; ++k) {
             p.h_pol.push_back(ho);
-            p.d_pol.push_back(dd);
             ho += (size_t)B * policy_sizes[k];
-            dd += (size_t)B * policy_sizes[k];
         }
         p.h_val = ho;
-        p.d_val = dd;
         const std::string ident = "gpu" + std::to_string(cfg->device) + "_p" + std::to_string(i);
         p.pool = gz_pool_create(sm, t, B, ident.c_str(), cfg->seed, cfg->game_index_base + (long)i * B, nullptr,
                                 p.h_planes, p.h_pol.data(), p.h_val);
         if (!p.pool) {
             g_err = std::string("gz_pool_create: ") + gz_engine_last_error();
-            delete r;
+            gz_runner_destroy(r);
             return nullptr;
         }
     }
@@ -203,7 +313,8 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
 
 extern "C" int gz_runner_start(gz_runner* r) {
     r->stop = false;
-    for (int i = 0; i < r->cfg.num_threads; ++i) r->threads.emplace_back(thread_main, r, i);
+    r->launcher = std::thread(launcher_main, r);
+    for (int i = 0; i < r->cfg.num_threads; ++i) r->threads.emplace_back(engine_main, r, i);
     return 0;
 }
 
@@ -226,6 +337,25 @@ extern "C" int gz_runner_wait_batches(gz_runner* r, long total_batches, double t
     return 0;
 }
 
+// Block until at least `total_rows` leaf evaluations have completed.
+extern "C" int gz_runner_wait_rows(gz_runner* r, long total_rows, double timeout_s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    std::unique_lock<std::mutex> lk(r->m);
+    while (r->rows.load() < total_rows) {
+        if (r->failed.load()) {
+            g_err = r->fail_msg;
+            return -1;
+        }
+        r->cv.wait_for(lk, std::chrono::milliseconds(2));
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (timeout_s > 0 && el > timeout_s) {
+            g_err = "timeout";
+            return -2;
+        }
+    }
+    return 0;
+}
+
 extern "C" int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out) {
     std::memset(out, 0, sizeof(*out));
     out->batches = r->batches.load();
@@ -233,7 +363,9 @@ extern "C" int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out) {
     out->kernel_ms = r->kernel_us.load() / 1000.0;
     out->kernel_launches = r->launches.load();
     out->samples = r->samples_taken.load();
+    out->segments = r->segments.load();
     for (Pool& p : r->pools) {
+        if (!p.pool) continue;
         gz_pool_stats s;
         gz_pool_get_stats(p.pool, &s);   // counters are plain longs written by the owning thread
         out->games_completed += s.games_completed;
@@ -248,24 +380,31 @@ extern "C" int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out) {
 
 extern "C" int gz_runner_stop(gz_runner* r) {
     r->stop = true;
+    r->qcv.notify_all();
     for (std::thread& th : r->threads) th.join();
     r->threads.clear();
-    return r->failed.load() ? -1 : 0;
+    if (r->launcher.joinable()) r->launcher.join();   // drains the batches in flight
+    if (r->failed.load()) {
+        g_err = r->fail_msg;
+        return -1;
+    }
+    return 0;
 }
 
 extern "C" void gz_runner_destroy(gz_runner* r) {
     if (!r) return;
-    if (!r->threads.empty()) gz_runner_stop(r);
+    if (!r->threads.empty() || r->launcher.joinable()) gz_runner_stop(r);
     (void)hipSetDevice(r->cfg.device);
+    if (r->stream) (void)hipStreamSynchronize(r->stream);
     for (Pool& p : r->pools) {
         if (p.pool) gz_pool_destroy(p.pool);
-        if (p.stream) (void)hipStreamDestroy(p.stream);
-        if (p.ev0) (void)hipEventDestroy(p.ev0);
-        if (p.ev1) (void)hipEventDestroy(p.ev1);
         if (p.h_planes) (void)hipHostFree(p.h_planes);
         if (p.h_out) (void)hipHostFree(p.h_out);
-        if (p.d_planes) (void)hipFree(p.d_planes);
-        if (p.d_out) (void)hipFree(p.d_out);
     }
+    for (Batch& b : r->batches_ring) {
+        if (b.ev0) (void)hipEventDestroy(b.ev0);
+        if (b.ev1) (void)hipEventDestroy(b.ev1);
+    }
+    if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
 }

@@ -2,21 +2,26 @@
 replacement of the reference's per-batch Python poll loop (cppinterface.py:131-144 driven by
 distributed/worker.py:191).  Pools, coroutines, planes and NN launches are all native."""
 import ctypes
+import json
 
 from . import _native, cppinterface
 
 
 class SelfPlayRunner(object):
     def __init__(self, hip_net, sm, transformer, conf, device=0, num_threads=8, pools_per_thread=2,
-                 batch_size=256, seed=0, game_index_base=0):
+                 batch_size=256, seed=0, game_index_base=0, keep_samples=False, max_launch_rows=0,
+                 spin_yield_playouts=0):
         self.lib = _native.runner_lib()
         _native.engine_lib()
         self.net = hip_net
         self.sm = sm
         self.c_transformer = cppinterface.create_c_transformer(transformer)
         self.cfg = _native.GzRunnerConfig(device, num_threads, pools_per_thread, batch_size, seed,
-                                          game_index_base, 1)
+                                          game_index_base, 1, int(keep_samples), max_launch_rows)
         self.conf = _native.make_selfplay_config(conf)
+        # build extension (engine/config.h): 0 keeps the reference's never-yielding playout loop
+        self.conf.puct_config.spin_yield_playouts = spin_yield_playouts
+        self.conf.run_to_end_puct_config.spin_yield_playouts = spin_yield_playouts
         ps = list(transformer.policy_dist_count)
         self._ps = (ctypes.c_int * len(ps))(*ps)
         self.handle = self.lib.gz_runner_create(hip_net.handle, sm.handle, self.c_transformer.handle,
@@ -34,6 +39,26 @@ class SelfPlayRunner(object):
         rc = self.lib.gz_runner_wait_batches(self.handle, total, timeout_s)
         if rc != 0:
             raise RuntimeError("runner wait failed (%d): %s" % (rc, self.lib.gz_runner_last_error().decode()))
+
+    def wait_rows(self, total, timeout_s=600.0, progress=None, interval_s=10.0):
+        """Block until `total` leaf evaluations completed; progress(stats) is called every
+        interval_s seconds while waiting (long runs print a heartbeat)."""
+        import time
+        t_end = time.time() + timeout_s
+        while True:
+            left = t_end - time.time()
+            rc = self.lib.gz_runner_wait_rows(self.handle, total, max(0.001, min(interval_s, left)))
+            if rc == 0:
+                return
+            if rc != -2 or time.time() >= t_end:
+                raise RuntimeError("runner wait failed (%d): %s" % (rc, self.lib.gz_runner_last_error().decode()))
+            if progress is not None:
+                progress(self.stats())
+
+    def fetch_samples(self):
+        """Samples produced since the last call (keep_samples=True), as datadesc.Sample dicts."""
+        s = _native.take_string(self.lib.gz_runner_fetch_samples(self.handle))
+        return json.loads(s) if s else []
 
     def stats(self):
         st = _native.GzRunnerStats()

@@ -54,6 +54,7 @@ typedef struct gz_puct_config {
     int backup_finalised;
     int lookup_transpositions;
     float evaluation_multiplier_to_convergence;
+    int spin_yield_playouts;     /* build extension, 0 = reference behaviour (engine/config.h) */
 } gz_puct_config;
 
 /* SelfPlayConfig (src/cpp/selfplay.h:19-41), filled from confs.SelfPlayConfig (confs.py:93-123)
@@ -175,6 +176,7 @@ int gz_pool_poll(gz_pool* p, int pred_count);   /* returns rows of planes now in
 int gz_pool_get_stats(gz_pool* p, gz_pool_stats* out);
 char* gz_pool_fetch_samples(gz_pool* p);          /* JSON or NULL; free with gz_free */
 long gz_pool_take_sample_count(gz_pool* p);       /* drops queued samples, returns how many */
+char* gz_pool_fetch_samples_n(gz_pool* p, long* count);  /* as fetch_samples, *count = records */
 
 #ifdef __cplusplus
 }

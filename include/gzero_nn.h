@@ -53,6 +53,20 @@ int gz_net_set_weights(gz_net* net, const float* blob, size_t count);
 /* Upload weights from a *device* float32 blob (e.g. after an RCCL broadcast into device memory). */
 int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_t count);
 
+/* One contiguous run of boards of a segmented launch.  Pointers may be device memory or pinned host
+ * memory (hipHostMalloc): the kernel gathers planes from, and scatters outputs to, each segment
+ * directly, so game pools need no staging copies. */
+#define GZ_MAX_SEGMENTS 32
+typedef struct gz_segment {
+    int rows;
+    const float* planes;                      /* [rows][C][H][W] */
+    float* policies[GZ_MAX_ROLES];            /* [rows][P_r] */
+    float* values;                            /* [rows][num_values] */
+} gz_segment;
+
+/* Asynchronous forward of up to GZ_MAX_SEGMENTS segments as ONE kernel launch on `stream`. */
+int gz_net_forward_segments(gz_net* net, void* stream, const gz_segment* segs, int nseg);
+
 /* Synchronous forward, host buffers: planes float32 [n][C][H][W] (the poll() buffer layout,
  * cppinterface.py:114); policies[r] float32 [n][P_r]; values float32 [n][num_values].
  * Equivalent of predict_on_batch on one batch. */
@@ -71,11 +85,18 @@ double gz_net_flops_per_eval(const gz_net* net);
 
 const char* gz_nn_last_error(void);
 
+/* Diagnostics: with GZ_KERNEL_STAMPS set in the environment, gz_net_forward records per-workgroup
+ * s_memtime stamps at phase boundaries; out8[1..5] = mean cycles of (input + initial conv,
+ * residual trunk, head 1x1 convs, policy dense + softmax, value head) of the last call. */
+int gz_net_stamp_avg(const gz_net* net, double* out8);
+
 /* ---- native self-play driver (runner.hip) ----------------------------------------------------
  * Replaces the Python poll loop of the reference (cppinterface.py:131-144 driven by
  * distributed/worker.py:191) and its worker threads (supervisor.cpp:79-99,196-245) for the
- * steady state: num_threads host threads x pools_per_thread game pools x batch_size games, one HIP
- * stream per pool, planes / predictions in pinned host memory, the fused forward on the stream.
+ * steady state: num_threads engine threads x pools_per_thread game pools x batch_size games; one
+ * launcher thread merges the pools waiting for predictions into segmented launches
+ * (gz_net_forward_segments) that read planes from / write predictions to the pools' pinned host
+ * buffers directly.
  * Uses the engine C-ABI (include/gzero_engine.h) for the pools. */
 struct gz_sm;
 struct gz_transformer;
@@ -90,12 +111,14 @@ typedef struct gz_runner_config {
     unsigned long long seed;
     long game_index_base;        /* global index of the first game (multi-GPU sharding) */
     int per_pool_unique_states;  /* pools always own their duplicate filter here (deterministic) */
+    int keep_samples;            /* 1: queue samples for gz_runner_fetch_samples; 0: count and drop */
+    int max_launch_rows;         /* cap on rows merged into one launch (0: no cap beyond 32 pools) */
 } gz_runner_config;
 
 typedef struct gz_runner_stats {
     long batches;                /* NN forwards completed */
     long rows;                   /* leaf evaluations completed */
-    double kernel_ms;            /* summed forward-kernel device time (HIP events on pool streams) */
+    double kernel_ms;            /* summed forward-kernel device time (HIP events around each launch) */
     long kernel_launches;
     long games_completed;
     long games_with_samples;
@@ -104,6 +127,7 @@ typedef struct gz_runner_stats {
     long resigns;
     long aborts;
     long dupes;
+    long segments;               /* pools merged into launches, summed over launches */
 } gz_runner_stats;
 
 gz_runner* gz_runner_create(gz_net* net, const struct gz_sm* sm, const struct gz_transformer* t,
@@ -111,9 +135,13 @@ gz_runner* gz_runner_create(gz_net* net, const struct gz_sm* sm, const struct gz
                             const int* policy_sizes, int num_policies, int num_values);
 int gz_runner_start(gz_runner* r);
 int gz_runner_wait_batches(gz_runner* r, long total_batches, double timeout_s);
+int gz_runner_wait_rows(gz_runner* r, long total_rows, double timeout_s);
 int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out);
 int gz_runner_stop(gz_runner* r);
 void gz_runner_destroy(gz_runner* r);
+/* Samples queued since the last call, as one JSON array of datadesc.Sample records
+ * (supervisor_impl.cpp:75-118 field names), or NULL when none; free with gz_free. */
+char* gz_runner_fetch_samples(gz_runner* r);
 const char* gz_runner_last_error(void);
 
 #ifdef __cplusplus

@@ -64,12 +64,20 @@ def test_native_runner_runs(hip_device):
     net = HipNet(setup.desc, hip_device)
     net.set_weights(to_blob(setup.weights))
     r = SelfPlayRunner(net, setup.sm, setup.transformer, _conf(), device=hip_device, num_threads=2,
-                       pools_per_thread=2, batch_size=32, seed=3)
+                       pools_per_thread=2, batch_size=32, seed=3, keep_samples=True)
     r.start()
-    r.wait_batches(4000, timeout_s=240)
+    r.wait_rows(4000 * 32, timeout_s=240)
     r.stop()
     st = r.stats()
+    samples = r.fetch_samples()
     r.close()
-    assert st["batches"] >= 4000 and st["rows"] > 0
+    assert st["rows"] >= 4000 * 32 and st["batches"] > 0
     assert st["kernel_launches"] == st["batches"] and st["kernel_ms"] > 0
+    assert st["batches"] <= st["segments"] <= 4 * st["batches"]     # 4 pools, merged launches
     assert st["games_completed"] > 0
+    assert len(samples) == st["samples"] > 0
+    s0 = samples[0]
+    for key in ("state", "prev_states", "policies", "final_score", "depth", "game_length", "match_identifier",
+                "has_resigned", "resign_false_positive", "starting_sample_depth", "resultant_puct_score",
+                "resultant_puct_visits"):
+        assert key in s0, key
