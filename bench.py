@@ -27,8 +27,8 @@ PEAK_BF16_TFLOPS = 2500.0      # gfx950 dense bf16 MFMA (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=20000)
+    ap.add_argument("--warmup", type=int, default=20000)
     ap.add_argument("--threads", type=int, default=0, help="host threads per GPU (0: auto)")
     ap.add_argument("--pools", type=int, default=2, help="game pools per thread")
     ap.add_argument("--batch", type=int, default=256)
@@ -119,6 +119,7 @@ def main():
     from galvanise_zero_amd._native import HipNet
     from galvanise_zero_amd.nn.weights import random_weights, to_blob
     from galvanise_zero_amd.runner import SelfPlayRunner
+    from galvanise_zero_amd import shard
 
     torch.cuda.set_device(local_rank)
     if world > 1:
@@ -131,8 +132,7 @@ def main():
     blob = torch.empty(net.weight_count, dtype=torch.float32, device="cuda")
     if rank == 0:
         blob.copy_(torch.from_numpy(to_blob(random_weights(desc, 7921))))
-    if world > 1:
-        dist.broadcast(blob, src=0)
+    shard.broadcast_weights(blob, src=0)
     torch.cuda.synchronize()
     net.set_weights_device(blob.data_ptr(), net.weight_count)
 
@@ -140,7 +140,8 @@ def main():
     threads = args.threads or max(1, min(14, cpus // max(1, world) - 2))   # + launcher + main
     runner = SelfPlayRunner(net, sm, transformer, selfplay_conf(args.mode, args.evals), device=local_rank,
                             num_threads=threads, pools_per_thread=args.pools, batch_size=args.batch,
-                            seed=args.seed, game_index_base=rank * threads * args.pools * args.batch,
+                            seed=args.seed,
+                            game_index_base=shard.game_index_base(rank, threads * args.pools * args.batch),
                             spin_yield_playouts=args.spin_yield)
     npools = runner.num_pools
 
@@ -172,14 +173,10 @@ def main():
     elapsed = t1 - t0
 
     d = {k: s1[k] - s0[k] for k in s1}
-    vec = torch.tensor([d["rows"], d["batches"], d["games_completed"], d["games_with_samples"], d["samples"],
-                        d["kernel_ms"], d["kernel_launches"], d["segments"]], dtype=torch.float64, device="cuda")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(vec, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    rows, batches, games, games_s, samples, kms, launches, segments = vec.tolist()
-    T = tmax.item()
+    totals, T = shard.reduce_counters(
+        [d["rows"], d["batches"], d["games_completed"], d["games_with_samples"], d["samples"], d["kernel_ms"],
+         d["kernel_launches"], d["segments"], s1["games_completed"], s1["completed_game_evals"]], elapsed, device="cuda")
+    rows, batches, games, games_s, samples, kms, launches, segments, games_all, game_evals_all = totals
 
     if rank == 0:
         flops = desc.flops_per_eval()
@@ -191,6 +188,10 @@ def main():
             "value": rows / T,
             "unit": "leaf-evals/s",
             "games_per_sec": games / T,
+            # steady state: leaf-evals/s / mean NN evaluations per completed game (all games since start)
+            "games_per_sec_steady": (rows / T) / (game_evals_all / games_all) if games_all else None,
+            "evals_per_game": game_evals_all / games_all if games_all else None,
+            "games_completed_total": games_all,
             "sample_games_per_sec": games_s / T,
             "samples_per_sec": samples / T,
             "n_gpus": world,

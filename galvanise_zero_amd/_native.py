@@ -224,7 +224,7 @@ class GzPoolStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_long) for n in (
         "games_started", "games_completed", "games_with_samples", "samples", "no_samples", "dupes",
         "resigns", "false_positive_resigns0", "false_positive_resigns1", "early_run_to_ends",
-        "aborts_game_length", "evaluations", "polls")]
+        "aborts_game_length", "evaluations", "polls", "completed_game_evals")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -372,7 +372,7 @@ class GzRunnerStats(ctypes.Structure):
                 ("kernel_launches", ctypes.c_long), ("games_completed", ctypes.c_long),
                 ("games_with_samples", ctypes.c_long), ("samples", ctypes.c_long), ("no_samples", ctypes.c_long),
                 ("resigns", ctypes.c_long), ("aborts", ctypes.c_long), ("dupes", ctypes.c_long),
-                ("segments", ctypes.c_long)]
+                ("segments", ctypes.c_long), ("completed_game_evals", ctypes.c_long)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -111,6 +111,7 @@ static void to_stats(const PoolStats& s, gz_pool_stats* o) {
     o->aborts_game_length = s.aborts_game_length;
     o->evaluations = s.evaluations;
     o->polls = s.polls;
+    o->completed_game_evals = s.completed_game_evals;
 }
 
 // ---- JSON of samples (sampleToDict, supervisor_impl.cpp:75-118) ---------------------------------

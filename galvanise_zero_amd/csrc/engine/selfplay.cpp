@@ -205,6 +205,12 @@ void SelfPlay::playOnce() {
     resign0_false_positive_check_scores.clear();
     resign1_false_positive_check_scores.clear();
 
+    const long evals0 = pe->totalEvaluations();
+    auto completed = [&]() {
+        manager->getStats().games_completed++;
+        manager->getStats().completed_game_evals += pe->totalEvaluations() - evals0;
+    };
+
     pe->reset(0);
     PuctNode* node = pe->establishRoot(initial_state);
     GZ_ASSERT(!node->isTerminal());
@@ -213,13 +219,13 @@ void SelfPlay::playOnce() {
     node = collectSamples(node);
     if (game_samples.empty()) {
         manager->incrNoSamples();
-        manager->getStats().games_completed++;
+        completed();
         return;
     }
 
     std::vector<float> final_scores;
     const int game_depth = runToEnd(node, final_scores);
-    manager->getStats().games_completed++;
+    completed();
     if (game_depth == -1) {
         for (Sample* s : game_samples) delete s;
         game_samples.clear();

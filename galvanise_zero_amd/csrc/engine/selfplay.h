@@ -108,6 +108,7 @@ struct PoolStats {
     long aborts_game_length = 0;
     long evaluations = 0;          // NN rows requested
     long polls = 0;
+    long completed_game_evals = 0; // NN evaluations consumed by the games counted in games_completed
 };
 
 class SelfPlayManager {

@@ -161,6 +161,7 @@ PoolStats Supervisor::stats() {
         s.aborts_game_length += p.aborts_game_length;
         s.evaluations += p.evaluations;
         s.polls += p.polls;
+        s.completed_game_evals += p.completed_game_evals;
     }
     return s;
 }

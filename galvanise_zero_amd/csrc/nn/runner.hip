@@ -374,6 +374,7 @@ extern "C" int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out) {
         out->resigns += s.resigns;
         out->aborts += s.aborts_game_length;
         out->dupes += s.dupes;
+        out->completed_game_evals += s.completed_game_evals;
     }
     return r->failed.load() ? -1 : 0;
 }

@@ -81,3 +81,56 @@ class SelfPlayRunner(object):
             self.close()
         except Exception:
             pass
+
+
+class GamePool(object):
+    """One game pool (the reference's SelfPlayManager, selfplaymanager.cpp:22-159) over caller-owned
+    numpy buffers, polled from Python: the unit the native runner schedules, exposed for tests and
+    for CPU-side drivers.  poll(pred_count) consumes the predictions written into `policies` /
+    `values` for the previous batch and returns the number of rows of planes now in `planes`."""
+
+    def __init__(self, sm, transformer, conf, batch_size, identifier="pool", seed=0, game_index_base=0):
+        import numpy as np
+        self.lib = _native.engine_lib()
+        self.c_transformer = cppinterface.create_c_transformer(transformer)
+        t = transformer
+        self.planes = np.zeros((batch_size, t.num_channels, t.num_cols, t.num_rows), dtype=np.float32)
+        self.policies = [np.zeros((batch_size, p), dtype=np.float32) for p in t.policy_dist_count]
+        self.values = np.zeros((batch_size, t.num_rewards), dtype=np.float32)
+        fp = ctypes.POINTER(ctypes.c_float)
+        self._pol_ptrs = (fp * len(self.policies))(*[p.ctypes.data_as(fp) for p in self.policies])
+        self.handle = self.lib.gz_pool_create(sm.handle, self.c_transformer.handle, batch_size,
+                                              identifier.encode(), seed, game_index_base, None,
+                                              self.planes.ctypes.data_as(fp), self._pol_ptrs,
+                                              self.values.ctypes.data_as(fp))
+        if not self.handle:
+            raise RuntimeError("gz_pool_create: %s" % _native.engine_error())
+        self._conf = _native.make_selfplay_config(conf)
+        if self.lib.gz_pool_start(self.handle, ctypes.byref(self._conf)) < 0:
+            raise RuntimeError("gz_pool_start: %s" % _native.engine_error())
+
+    def poll(self, pred_count):
+        n = self.lib.gz_pool_poll(self.handle, pred_count)
+        if n < 0:
+            raise RuntimeError("gz_pool_poll: %s" % _native.engine_error())
+        return n
+
+    def fetch_samples(self):
+        s = _native.take_string(self.lib.gz_pool_fetch_samples(self.handle))
+        return json.loads(s) if s else []
+
+    def stats(self):
+        st = _native.GzPoolStats()
+        self.lib.gz_pool_get_stats(self.handle, ctypes.byref(st))
+        return st.as_dict()
+
+    def close(self):
+        if self.handle:
+            self.lib.gz_pool_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -94,6 +94,7 @@ typedef struct gz_pool_stats {
     long aborts_game_length;
     long evaluations;
     long polls;
+    long completed_game_evals;   /* NN evaluations consumed by the completed games */
 } gz_pool_stats;
 
 const char* gz_engine_last_error(void);

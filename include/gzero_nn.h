@@ -128,6 +128,7 @@ typedef struct gz_runner_stats {
     long aborts;
     long dupes;
     long segments;               /* pools merged into launches, summed over launches */
+    long completed_game_evals;   /* NN evaluations consumed by the completed games */
 } gz_runner_stats;
 
 gz_runner* gz_runner_create(gz_net* net, const struct gz_sm* sm, const struct gz_transformer* t,
