@@ -22,6 +22,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0      # gfx950 dense bf16 MFMA (MI355X_MICROARCH.md)
+# PMC-measured fabric bytes per trunk launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc
+# passes, tools/profile_bench.sh); None until measured for the current kernel.
+TRAFFIC_PER_LAUNCH = None
+TRAFFIC_SOURCE = None
 
 
 def parse():
@@ -175,14 +179,16 @@ def main():
     d = {k: s1[k] - s0[k] for k in s1}
     totals, T = shard.reduce_counters(
         [d["rows"], d["batches"], d["games_completed"], d["games_with_samples"], d["samples"], d["kernel_ms"],
-         d["kernel_launches"], d["segments"], s1["games_completed"], s1["completed_game_evals"]], elapsed, device="cuda")
-    rows, batches, games, games_s, samples, kms, launches, segments, games_all, game_evals_all = totals
+         d["kernel_launches"], d["segments"], s1["games_completed"], s1["completed_game_evals"], d["trunk_ms"]],
+        elapsed, device="cuda")
+    rows, batches, games, games_s, samples, kms, launches, segments, games_all, game_evals_all, tms = totals
 
     if rank == 0:
         flops = desc.flops_per_eval()
-        avg_kernel_s = (kms / launches) / 1e3 if launches else float("nan")
+        avg_fwd_s = (kms / launches) / 1e3 if launches else float("nan")
+        avg_trunk_s = (tms / launches) / 1e3 if launches else float("nan")
         rows_per_launch = rows / launches if launches else float("nan")
-        achieved = flops * rows_per_launch / avg_kernel_s / 1e12
+        achieved = desc.flops_trunk() * rows_per_launch / avg_trunk_s / 1e12
         out = {
             "metric": "self-play games/sec + NN leaf-evals/sec, breakthrough 8x8 @ 800 playouts/move",
             "value": rows / T,
@@ -208,9 +214,13 @@ def main():
                        "games_per_gpu": npools * args.batch, "threads_per_gpu": threads,
                        "pools_per_thread": args.pools, "eval_batch": args.batch, "parallelism": "games sharded dp%d" % world},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": None,
-                         "kernel": "gznn::forward_kernel<128,8,8>", "avg_kernel_ms": avg_kernel_s * 1e3,
-                         "rows_per_launch": rows_per_launch, "pools_per_launch": segments / launches if launches else None,
+                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": TRAFFIC_PER_LAUNCH,
+                         "traffic_source": TRAFFIC_SOURCE,
+                         "kernel": "gznn::trunk_kernel<128,8,8,1,2>", "avg_kernel_ms": avg_trunk_s * 1e3,
+                         "flop_per_leaf_kernel": desc.flops_trunk(), "rows_per_launch": rows_per_launch,
+                         "pools_per_launch": segments / launches if launches else None,
+                         "forward_avg_ms": avg_fwd_s * 1e3,
+                         "forward_tflops": flops * rows_per_launch / avg_fwd_s / 1e12,
                          "flop_per_leaf": flops, "aggregate_tflops": flops * rows / T / 1e12},
             "gpu_busy_frac": (kms / 1e3) / (T * world) if T > 0 else None,
         }

@@ -369,6 +369,7 @@ class GzRunnerConfig(ctypes.Structure):
 
 class GzRunnerStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_long), ("rows", ctypes.c_long), ("kernel_ms", ctypes.c_double),
+                ("trunk_ms", ctypes.c_double),
                 ("kernel_launches", ctypes.c_long), ("games_completed", ctypes.c_long),
                 ("games_with_samples", ctypes.c_long), ("samples", ctypes.c_long), ("no_samples", ctypes.c_long),
                 ("resigns", ctypes.c_long), ("aborts", ctypes.c_long), ("dupes", ctypes.c_long),

@@ -1,17 +1,34 @@
-// Fused whole-network forward of the v1 residual policy/value CNN for gfx950 (MI355X).
+// Forward of the v1 residual policy/value CNN for gfx950 (MI355X): two launches per batch.
 //
-// One workgroup (4 waves) evaluates NB boards end to end:
-//   planes (fp32 NCHW, HBM) -> im2col in LDS -> initial conv -> B residual blocks -> heads
-//   -> softmax policies / value (fp32, HBM).
-// Trunk activations never leave the CU: the bf16 copy that feeds the next conv lives in LDS
-// (two ping-pong images), the fp32 residual stream lives in the MFMA accumulator registers.
-// Weights (bf16, BN folded, MFMA-fragment packed) stream from L2 straight into VGPRs.
+// trunk_kernel: one workgroup (4 waves) evaluates NB boards through the whole trunk:
+//   planes (fp32 NCHW, HBM or pinned host) -> im2col in LDS -> initial conv -> B residual blocks
+//   -> the heads' 1x1 convs -> per-board head features (fp32) to a device scratch.
+//   Trunk activations never leave the CU: the bf16 copy that feeds the next conv lives in LDS
+//   (two ping-pong images per board), the fp32 residual stream lives in the MFMA accumulators.
+// heads_kernel: one workgroup takes BPW boards' features and applies the policy Dense + softmax
+//   and value MLP + softmax in fp32 with the dense weights read once per BPW boards; the results go
+//   straight to the callers' buffers (segments).
 //
 // Each 3x3 conv is an implicit GEMM  out[co][p] = sum_{tap,ci} W[co][tap,ci] * X[nbr(p,tap)][ci]
-// on v_mfma_f32_16x16x32_bf16 with A = weights (rows co), B = activations (cols = positions), so
-// the accumulator of a lane holds 4 consecutive channels of one position and the epilogue is one
-// 8-byte LDS store.  Wave w owns output channels [w*F/4, (w+1)*F/4) for every position of the
-// workgroup's NB boards, so one weight fragment (16 B/lane from L2) feeds NB*ceil(HW/16) MFMAs.
+// on v_mfma_f32_16x16x32_bf16, A = weights (rows co), B = activations (cols = positions).  Wave w
+// owns output channels [w*F/4, (w+1)*F/4) for every position of the NB boards, so one weight
+// fragment feeds NB*ceil(HW/16) MFMAs.
+//
+// Weight stream: every trunk conv's weights (bf16, BN folded, MFMA-fragment order) are one
+// contiguous stream that each wave walks in "stages" of KS k-steps.  Stages land in a ring of R
+// register slots, issued R-1 stages ahead by inline-asm loads the compiler cannot sink and counted
+// with explicit s_waitcnt vmcnt(N): the ring runs continuously across conv boundaries and is primed
+// before the input stage, so the L2/Infinity-Cache latency of the weight stream (~1 us when every
+// CU streams) is covered by R-1 stages of MFMA work instead of one.
+//
+// LDS images: row q (a board position, plus one all-zero row) is ROWS = 512 bytes and holds the F
+// bf16 channels as 16-byte chunks, logical chunk L at physical chunk L + s(q), s(q) = 2q mod 16
+// (a rotation without wrap-around: the row has room for chunks 0 .. F/8+13).  The 4-bank group of
+// a chunk is its index mod 16, so the two k-slices a ds_read_b128 lane group pairs (g, g^1) land on
+// opposite parities and the 16 lanes of a group hit 16 distinct bank groups for every 3x3 shift;
+// out-of-board neighbours read the zero row at the chunk of their virtual (unclipped) position,
+// which keeps them conflict-free too.  Because the rotation adds, the k-steps of one tap differ by
+// a constant byte offset: one address register per (tap, position tile) serves all of them.
 //
 // Reference semantics: src/ggpzero/nn/model.py:25-75, 154-296 (see oracle/nn_ref.py).
 #pragma once
@@ -19,10 +36,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 namespace gznn {
 
 constexpr int kMaxRoles = 4;
 constexpr int kMaxSegments = 32;
+constexpr int kHeadBoards = 4;     // boards per heads_kernel workgroup (one softmax wave per board)
 
 // One contiguous run of boards of a launch: its planes and outputs may live anywhere the device
 // can address (HBM, or pinned host memory of a game pool: zero-copy gather / scatter).
@@ -43,21 +63,31 @@ struct KParams {
     const float* bres;       // [2B][F]
     const float* wh;         // head 1x1 convs (BN folded) [2R+1][F]
     const float* bh;         // [2R+1]
-    const float* pd[kMaxRoles];   // policy dense, transposed [P_r][2HW]
+    const float* pd[kMaxRoles];   // policy dense, Keras layout [2HW][P_r] (k-major)
     const float* pb[kMaxRoles];   // [P_r]
-    const float* vhw;        // value hidden, transposed [VH][HW]
+    const float* vhw;        // value hidden, Keras layout [HW][VH]
     const float* vhb;        // [VH]
     const float* vdw;        // value dense [VH][V]
     const float* vdb;        // [V]
+    float* feat;             // scratch [n][HC*HW]: head features in flatten order (trunk -> heads)
     int n;                   // boards in this launch
     int nseg;                // segments (>= 1), ascending row0, seg[0].row0 == 0
     Segment seg[kMaxSegments];
     unsigned long long* stamps;   // diagnostics only (GZ_KERNEL_STAMPS): [grid][8] s_memtime per phase
-    int C, K0, B, R, VH, V, leaky, flatten_nchw, maxP;
+    int C, K0, B, R, VH, V, leaky, flatten_nchw, maxP, npos;
+    int btab_off;            // LDS byte offset of the trunk bias table
     int P[kMaxRoles];
 };
 
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
+
+// ring depth: largest R dividing the stages per conv with R slots of KS*CT fragments <= 96 VGPRs
+__host__ __device__ constexpr int ring_depth(int nst, int ks, int ct) {
+    const int cand[5] = {9, 6, 4, 3, 2};
+    for (int i = 0; i < 5; ++i)
+        if (nst % cand[i] == 0 && cand[i] * ks * ct * 4 <= 96 && (cand[i] - 1) * ks * ct <= 60) return cand[i];
+    return 1;
+}
 
 template <int F, int H, int W, int NB = 1>
 struct Geo {
@@ -66,21 +96,30 @@ struct Geo {
     static constexpr int TT = NB * PT;               // position tiles per wave (all boards)
     static constexpr int CT = F / 64;                // co tiles per wave (MFMA M)
     static constexpr int KC = F / 32;                // k-steps per tap
-    static constexpr int ROWB = F * 2;               // bytes per LDS activation row
-    static constexpr int CPR = F / 8;                // 16-byte chunks per row
-    static constexpr int SWZ = (CPR < 16 ? CPR : 16) - 1;
-    static constexpr int ACT_BYTES = align16((NPOS + 1) * ROWB);   // + one all-zero row
+    static constexpr int CPR = F / 8;                // 16-byte chunks of channels per row
+    static constexpr int ROWS = ((CPR + 14) * 16 + 255) & ~255;   // LDS row stride (rotated chunks)
+    static constexpr int ACT_BYTES = (NPOS + 1) * ROWS;           // + one all-zero row
+    static constexpr int KS = 2;                     // k-steps per ring stage
+    static constexpr int NST = 9 * KC / KS;          // ring stages per conv
+    static constexpr int R = ring_depth(NST, KS, CT);
+    static constexpr int LPS = KS * CT;              // weight loads per stage per lane
     static_assert(F % 64 == 0, "filters must be a multiple of 64");
+    static_assert(KC % KS == 0, "a stage must not straddle a tap");
+    static_assert(R >= 2, "no ring depth fits");
 };
 
-// Scratch bytes needed beyond the two activation images (host and device agree on this).
-__host__ __device__ inline int scratch_bytes(int npos, int C, int K0, int R, int maxP, int VH) {
-    int in_stage = align16(C * npos * 4) + align16((npos + 1) * K0 * 2);
-    int hc = 2 * R + 1;
-    int heads = align16(4 * hc * npos * 4) + align16(hc * npos * 4)
-              + align16((maxP > VH ? maxP : VH) * 4) + 64 * 4;
+// chunk rotation of LDS row q (q may be a virtual, off-board position)
+__device__ __forceinline__ int swz(int q) { return (2 * q) & 14; }
+
+// LDS bytes of the trunk kernel beyond the two activation image sets: bias table + scratch
+// (input staging / 1x1-head partials; the scratch aliases the second image set).
+__host__ __device__ inline int trunk_scratch_bytes(int npos, int C, int K0, int R) {
+    const int in_stage = align16(C * npos * 4) + align16((npos + 1) * K0 * 2);
+    const int hc = 2 * R + 1;
+    const int heads = align16(4 * hc * npos * 4);
     return in_stage > heads ? in_stage : heads;
 }
+__host__ __device__ inline int bias_table_bytes(int F, int B) { return align16((2 * B) * F * 4); }
 
 __device__ __forceinline__ float act_fn(float v, int leaky) {
     return v > 0.f ? v : (leaky ? 0.03f * v : 0.f);
@@ -98,7 +137,7 @@ __device__ __forceinline__ void store_act(char* X, int p, int co, f32x4 v) {
         uint2 u;
         u.x = pack2(v[0], v[1]);
         u.y = pack2(v[2], v[3]);
-        *(uint2*)(X + p * G::ROWB + ((((co >> 3) ^ (p & G::SWZ))) << 4) + (co & 7) * 2) = u;
+        *(uint2*)(X + p * G::ROWS + (((co >> 3) + swz(p)) << 4) + (co & 7) * 2) = u;
     }
 }
 
@@ -114,179 +153,160 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
-// Workgroup reduction through an LDS slot per wave; all threads get the result.
-template <bool IS_MAX, int NWAVES>
-__device__ __forceinline__ float block_reduce(float v, float* red) {
-    v = IS_MAX ? wave_max(v) : wave_sum(v);
-    const int wave = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[wave] = v;
-    __syncthreads();
-    float r = red[0];
-#pragma unroll
-    for (int w = 1; w < NWAVES; ++w) r = IS_MAX ? fmaxf(r, red[w]) : r + red[w];
-    return r;
-}
-
 __device__ __forceinline__ int find_segment(const KParams& kp, int board) {
     int s = 0;
     while (s + 1 < kp.nseg && board >= kp.seg[s + 1].row0) ++s;
     return s;
 }
 
-// out[j] = bias[j] + sum_i WT[j][i] * x[i] for j < rows (x in LDS, WT row-major in global, fp32):
-// 16 lanes per output row, 4 rows per wave, so every load instruction reads four 64-byte runs and
-// each row's partial sums meet in a 4-step shuffle.  U row groups are in flight per wave at once:
-// the loads of a group are independent, and issuing U*K/16 of them back to back turns U L2 round
-// trips into one.
-template <int K, int NWAVES>
-__device__ __forceinline__ void dense_rows(const float* __restrict__ WT, const float* __restrict__ bias, int rows,
-                                           const float* __restrict__ x, float* __restrict__ out, int wave, int lane) {
-    constexpr int U = K <= 64 ? 8 : 4;
-    constexpr int NI = (K + 15) / 16;
-    const int l16 = lane & 15, sub = lane >> 4;
-    float xv[NI];
-#pragma unroll
-    for (int n = 0; n < NI; ++n) xv[n] = (l16 + 16 * n < K) ? x[l16 + 16 * n] : 0.f;
-    for (int j0 = 4 * wave + sub; j0 < rows; j0 += 4 * NWAVES * U) {
-        float s[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int j = j0 + u * 4 * NWAVES;
-            const float* wr = WT + (size_t)(j < rows ? j : 0) * K;
-            s[u] = 0.f;
-#pragma unroll
-            for (int n = 0; n < NI; ++n)
-                if (l16 + 16 * n < K) s[u] += wr[l16 + 16 * n] * xv[n];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            float v = s[u];
-            v += __shfl_xor(v, 8, 64);
-            v += __shfl_xor(v, 4, 64);
-            v += __shfl_xor(v, 2, 64);
-            v += __shfl_xor(v, 1, 64);
-            const int j = j0 + u * 4 * NWAVES;
-            if (l16 == 0 && j < rows) out[j] = v + bias[j];
-        }
-    }
-}
-
-// Weight prefetch that the compiler cannot move: issued as inline asm at the top of an iteration
-// and consumed after an explicit vmcnt(0) at its end.  (Plain loads get sunk past the loop back
-// edge to right before their first MFMA, which exposes the whole L2 latency every iteration.)
-// The compiler does not track these loads, so gload_wait_all must precede any use of the result;
-// gload_ready then re-defines each register after the wait so no copy can be hoisted above it.
-__device__ __forceinline__ bf16x8 gload_issue(const __bf16* p) {
+// Weight-stream loads the compiler cannot move: issued as inline asm, consumed after an explicit
+// s_waitcnt vmcnt(N).  The compiler does not track these loads, so ring_wait must precede any use
+// of the result; ring_ready then re-defines each register after the wait so no use (or copy) can be
+// hoisted above it.  Every issued register stays live until consumed or until ring_drain.
+template <int IMM>
+__device__ __forceinline__ bf16x8 gload_issue(uint32_t voff, const void* sbase) {
     bf16x8 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(v) : "v"(voff), "s"(sbase), "n"(IMM) : "memory");
     return v;
 }
-__device__ __forceinline__ void gload_wait_all(bf16x8& v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)::"memory"); }
-__device__ __forceinline__ void gload_ready(bf16x8& v) { asm volatile("" : "+v"(v)); }
+template <int N>
+__device__ __forceinline__ void ring_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ void ring_ready(bf16x8& v) { asm volatile("" : "+v"(v)); }
+
+// ---- trunk -------------------------------------------------------------------------------------
+
+template <int F, int H, int W, int NB>
+struct Ring {
+    using G = Geo<F, H, W, NB>;
+    bf16x8 r[G::R][G::KS][G::CT];
+};
+
+// Issue stage `gs` of the trunk weight stream (clamped to the last stage) into ring slot SLOT.
+// Fragment (step, ct) of a lane: wres + (step*F + 16ct)*64 bytes + woff, woff = lane's row/slice;
+// the stage base is scalar, ct is the instruction's immediate offset.
+template <int F, int H, int W, int NB, int SLOT, int... CTS>
+__device__ __forceinline__ void ring_issue_k(Ring<F, H, W, NB>& ring, int k, uint32_t woff, const char* sb,
+                                             std::integer_sequence<int, CTS...>) {
+    ((ring.r[SLOT][k][CTS] = gload_issue<CTS * 16 * 64>(woff, sb)), ...);
+}
+template <int F, int H, int W, int NB, int SLOT>
+__device__ __forceinline__ void ring_issue(Ring<F, H, W, NB>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
+    using G = Geo<F, H, W, NB>;
+    const int s = gs < gmax ? gs : gmax;
+#pragma unroll
+    for (int k = 0; k < G::KS; ++k)
+        ring_issue_k<F, H, W, NB, SLOT>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * 64,
+                                        std::make_integer_sequence<int, G::CT>{});
+}
+
+// LDS byte offset (within a board image) of a lane's B fragment for tap `tap`, position tile pt,
+// k-step 0 of the tap; k-step kc adds kc*64.  Callers launder `lane` (an empty asm redefinition)
+// once per tap so these offsets are computed when the tap starts instead of being hoisted for all
+// nine taps out of the trunk loop, which would pin 9*PT address registers for the whole kernel.
+__device__ __forceinline__ void launder(int& v) { asm volatile("" : "+v"(v)); }
+template <int F, int H, int W>
+__device__ __forceinline__ int tap_base(int tap, int pt, int lane) {
+    using G = Geo<F, H, W>;
+    const int li = lane & 15, g = lane >> 4;
+    const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+    const int p = 16 * pt + li;
+    const int y = p / W + dy, x = p % W + dx;
+    const bool ok = p < G::NPOS && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    const int qv = p + dy * W + dx;
+    return (ok ? qv : G::NPOS) * G::ROWS + ((g + swz(qv)) << 4);
+}
 
 // One 3x3 'same' conv over the NB LDS images at X (board b at X + b*ACT_BYTES):
-// acc[ct][t] = W * X (fp32 accumulate), tile t = b*PT + pt.  Every weight fragment loaded from L2
-// feeds TT = NB*PT MFMAs -- NB is the weight-reuse factor that sets the L2->CU byte rate.
-template <int F, int H, int W, int NB>
-__device__ __forceinline__ void conv3x3(const char* __restrict__ X, const __bf16* __restrict__ wp,
-                                        f32x4 (&acc)[Geo<F, H, W>::CT][Geo<F, H, W, NB>::TT],
-                                        int co_base, int li, int g) {
+// acc[ct][t] = W * X (fp32 accumulate), tile t = b*PT + pt.  gs0 = global stage index of this
+// conv's first stage; on entry stages gs0 .. gs0+R-2 are in flight in ring slots 0..R-2.
+template <int F, int H, int W, int NB, int ST>
+__device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, H, W, NB>& ring,
+                                           f32x4 (&acc)[Geo<F, H, W, NB>::CT][Geo<F, H, W, NB>::TT],
+                                           bf16x8 (&b)[2][Geo<F, H, W, NB>::TT], const __bf16* wres, uint32_t woff,
+                                           int gs0, int gmax, int& lane) {
     using G = Geo<F, H, W, NB>;
-    constexpr int CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC;
-    // The k loop runs as 9*KC/KS rolled iterations of KS k-steps (KS | KC, a tap or part of one).
-    // Each iteration first issues the weight fragments of the NEXT iteration (one full iteration
-    // of MFMAs hides their L2 latency), and double-buffers the activation fragments from LDS one
-    // k-step ahead.  A rolled loop keeps the LDS address math out of registers.
-    constexpr int KS = KC < 4 ? KC : 4;
-    constexpr int NIT = 9 * KC / KS;
-    static_assert(KC % KS == 0, "k-steps per iteration must divide the k-steps per tap");
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-        for (int t = 0; t < TT; ++t) acc[ct][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // lane's fragment of step s = tap*KC + kc: wp + ((s*F + co_base + 16ct + li) * 32 + 8g)
-    const __bf16* wl = wp + (size_t)(co_base + li) * 32 + 8 * g;
-    bf16x8 cur[KS][CT];
+    constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC;
+    // refill the slot stage ST-1 consumed with stage ST+R-1, then wait for stage ST
+    ring_issue<F, H, W, NB, (ST + R - 1) % R>(ring, wres, woff, gs0 + ST + R - 1, gmax);
+    ring_wait<(R - 1) * G::LPS>();
 #pragma unroll
     for (int k = 0; k < KS; ++k)
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-            cur[k][ct] = *(const bf16x8*)(wl + ((size_t)k * F + 16 * ct) * 32);
-    // land the first fragments before the loop so the loop header carries no pending loads
-#pragma unroll
-    for (int k = 0; k < KS; ++k)
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) gload_ready(cur[k][ct]);
+        for (int ct = 0; ct < CT; ++ct) ring_ready(ring.r[ST % R][k][ct]);
 
-#pragma unroll 1
-    for (int it = 0; it < NIT; ++it) {
-        const int itn = it + 1 < NIT ? it + 1 : it;     // the last iteration re-reads its own
-        bf16x8 nxt[KS][CT];
 #pragma unroll
-        for (int k = 0; k < KS; ++k)
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct)
-                nxt[k][ct] = gload_issue(wl + ((size_t)(itn * KS + k) * F + 16 * ct) * 32);
-
-        const int s0 = it * KS;
-        const int tap = s0 / KC, kc0 = s0 % KC;
-        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-        int qoff[PT], qswz[PT];
-#pragma unroll
-        for (int pt = 0; pt < PT; ++pt) {
-            const int p = 16 * pt + li;
-            const int y = p / W + dy, x = p % W + dx;
-            const bool ok = p < G::NPOS && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-            const int q = ok ? p + dy * W + dx : G::NPOS;
-            qoff[pt] = q * G::ROWB;
-            qswz[pt] = q & G::SWZ;
-        }
-        bf16x8 b[2][TT];
-        auto load_b = [&](int kc, bf16x8 (&dst)[TT]) {
+    for (int k = 0; k < KS; ++k) {
+        const int j = ST * KS + k;             // k-step within the conv
+        if (j + 1 < 9 * KC) {                  // B fragments of the next k-step (double buffer)
+            const int jn = j + 1;
+            const int tap = jn / KC, kc = jn % KC;
+            if (kc == 0) launder(lane);
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) {
-                const int off = qoff[pt] + (((kc * 4 + g) ^ qswz[pt]) << 4);
+                const char* a = X + tap_base<F, H, W>(tap, pt, lane) + kc * 64;
 #pragma unroll
-                for (int bb = 0; bb < NB; ++bb) dst[bb * PT + pt] = *(const bf16x8*)(X + bb * G::ACT_BYTES + off);
+                for (int bb = 0; bb < NB; ++bb) b[jn & 1][bb * PT + pt] = *(const bf16x8*)(a + bb * G::ACT_BYTES);
             }
-        };
-        load_b(kc0, b[0]);
-#pragma unroll
-        for (int k = 0; k < KS; ++k) {
-            if (k + 1 < KS) load_b(kc0 + k + 1, b[(k + 1) & 1]);
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-                for (int t = 0; t < TT; ++t)
-                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[k][ct], b[k & 1][t], acc[ct][t], 0, 0, 0);
         }
-        // the prefetched fragments have had a whole iteration to land
-        gload_wait_all(nxt[0][0]);
 #pragma unroll
-        for (int k = 0; k < KS; ++k)
+        for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                gload_ready(nxt[k][ct]);
-                cur[k][ct] = nxt[k][ct];
-            }
+            for (int t = 0; t < TT; ++t)
+                acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring.r[ST % R][k][ct], b[j & 1][t], acc[ct][t], 0, 0, 0);
     }
+}
+
+template <int F, int H, int W, int NB, int... S>
+__device__ __forceinline__ void ring_prime(Ring<F, H, W, NB>& ring, const __bf16* wres, uint32_t woff, int gmax,
+                                           std::integer_sequence<int, S...>) {
+    (ring_issue<F, H, W, NB, S>(ring, wres, woff, S, gmax), ...);
+}
+
+template <int F, int H, int W, int NB, int... ST>
+__device__ __forceinline__ void conv_stages(const char* __restrict__ X, Ring<F, H, W, NB>& ring,
+                                            f32x4 (&acc)[Geo<F, H, W, NB>::CT][Geo<F, H, W, NB>::TT],
+                                            bf16x8 (&b)[2][Geo<F, H, W, NB>::TT], const __bf16* wres,
+                                            uint32_t woff, int gs0, int gmax, int& lane,
+                                            std::integer_sequence<int, ST...>) {
+    (conv_stage<F, H, W, NB, ST>(X, ring, acc, b, wres, woff, gs0, gmax, lane), ...);
+}
+
+template <int F, int H, int W, int NB>
+__device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, H, W, NB>& ring,
+                                        f32x4 (&acc)[Geo<F, H, W, NB>::CT][Geo<F, H, W, NB>::TT],
+                                        const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane) {
+    using G = Geo<F, H, W, NB>;
+    constexpr int PT = G::PT, TT = G::TT;
+#pragma unroll
+    for (int ct = 0; ct < G::CT; ++ct)
+#pragma unroll
+        for (int t = 0; t < TT; ++t) acc[ct][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 b[2][TT];
+    // k-step 0 = tap 0 (dy = dx = -1), kc 0
+    launder(lane);
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) {
+        const char* a = X + tap_base<F, H, W>(0, pt, lane);
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) b[0][bb * PT + pt] = *(const bf16x8*)(a + bb * G::ACT_BYTES);
+    }
+    conv_stages<F, H, W, NB>(X, ring, acc, b, wres, woff, gs0, gmax, lane, std::make_integer_sequence<int, G::NST>{});
 }
 
 // NB boards per workgroup of 4 waves; WPE = minimum resident waves per SIMD the register
 // allocation must allow (amdgpu_waves_per_eu), i.e. WPE workgroups per CU.
 template <int F, int H, int W, int NB, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
-forward_kernel(const KParams kp) {
+trunk_kernel(const KParams kp) {
     using G = Geo<F, H, W, NB>;
-    constexpr int NPOS = G::NPOS, PT = G::PT, TT = G::TT, CT = G::CT, kThreads = 256;
+    constexpr int NPOS = G::NPOS, PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, kThreads = 256;
     constexpr int ACT = G::ACT_BYTES;
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* X0 = smem;                 // [NB][ACT]
     char* X1 = smem + NB * ACT;      // [NB][ACT]
     char* SCR = X1;                  // scratch aliases X1 while X1 holds no live activations
+    float* btab = (float*)(smem + kp.btab_off);   // trunk conv biases [2B][F], after X1 / scratch
 
     const int board0 = blockIdx.x * NB;
     const int tid = threadIdx.x;
@@ -299,12 +319,19 @@ forward_kernel(const KParams kp) {
     const int co_base = wave * (F / 4);
     const int C = kp.C, K0 = kp.K0;
 
+    // prime the weight ring: stages 0 .. R-2 of the trunk stream
+    const uint32_t woff = (uint32_t)((co_base + li) * 64 + 16 * g);   // lane's fragment bytes within a k-step
+    const int gmax = 2 * kp.B * G::NST - 1;
+    Ring<F, H, W, NB> ring;
+    if (kp.B > 0) ring_prime<F, H, W, NB>(ring, kp.wres, woff, gmax, std::make_integer_sequence<int, R - 1>{});
+
     f32x4 acc[CT][TT];
     f32x4 resid[CT][TT];
 
-    for (int i = tid; i < NB * G::ROWB / 4; i += kThreads) {
-        const int bb = i / (G::ROWB / 4), j = i % (G::ROWB / 4);
-        ((uint32_t*)(X0 + bb * ACT + NPOS * G::ROWB))[j] = 0u;
+    for (int i = tid; i < 2 * kp.B * F; i += kThreads) btab[i] = kp.bres[i];
+    for (int i = tid; i < NB * G::ROWS / 4; i += kThreads) {
+        const int bb = i / (G::ROWS / 4), j = i % (G::ROWS / 4);
+        ((uint32_t*)(X0 + bb * ACT + NPOS * G::ROWS))[j] = 0u;
     }
 
     // ---- per board: stage planes, im2col, initial conv (GEMM over K0) ----------------------
@@ -349,11 +376,11 @@ forward_kernel(const KParams kp) {
             for (int pt = 0; pt < PT; ++pt) {
                 const int p = 16 * pt + li;
                 const int q = p < NPOS ? p : NPOS;
-                const bf16x8 b = *(const bf16x8*)(IM + q * imrow + ((((s * 4 + g)) ^ (q & imswz)) << 4));
+                const bf16x8 bq = *(const bf16x8*)(IM + q * imrow + ((((s * 4 + g)) ^ (q & imswz)) << 4));
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct)
                     acc[ct][bb * PT + pt] =
-                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], b, acc[ct][bb * PT + pt], 0, 0, 0);
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], bq, acc[ct][bb * PT + pt], 0, 0, 0);
             }
         }
 #pragma unroll
@@ -373,22 +400,19 @@ forward_kernel(const KParams kp) {
         }
         __syncthreads();    // scratch is reused by the next board
     }
-    for (int i = tid; i < NB * G::ROWB / 4; i += kThreads) {
-        const int bb = i / (G::ROWB / 4), j = i % (G::ROWB / 4);
-        ((uint32_t*)(X1 + bb * ACT + NPOS * G::ROWB))[j] = 0u;
+    for (int i = tid; i < NB * G::ROWS / 4; i += kThreads) {
+        const int bb = i / (G::ROWS / 4), j = i % (G::ROWS / 4);
+        ((uint32_t*)(X1 + bb * ACT + NPOS * G::ROWS))[j] = 0u;
     }
     __syncthreads();
 
     GZ_STAMP(1);
     // ---- residual tower ------------------------------------------------------------------
-    constexpr size_t conv_elems = (size_t)9 * F * F;
     for (int blk = 0; blk < kp.B; ++blk) {
-        const __bf16* w_a = kp.wres + (size_t)(2 * blk) * conv_elems;
-        const __bf16* w_b = w_a + conv_elems;
-        const float* b_a = kp.bres + (size_t)(2 * blk) * F;
+        const float* b_a = btab + (2 * blk) * F;
         const float* b_b = b_a + F;
 
-        conv3x3<F, H, W, NB>(X0, w_a, acc, co_base, li, g);
+        conv3x3<F, H, W, NB>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -405,7 +429,7 @@ forward_kernel(const KParams kp) {
         }
         __syncthreads();
 
-        conv3x3<F, H, W, NB>(X1, w_b, acc, co_base, li, g);
+        conv3x3<F, H, W, NB>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -424,21 +448,25 @@ forward_kernel(const KParams kp) {
         }
         __syncthreads();
     }
+    // the clamped tail stages are never consumed: land them before their registers are released
+    if (kp.B > 0) {
+        ring_wait<0>();
+#pragma unroll
+        for (int s = 0; s < R; ++s)
+#pragma unroll
+            for (int k = 0; k < G::KS; ++k)
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) ring_ready(ring.r[s][k][ct]);
+    }
 
     GZ_STAMP(2);
-    // ---- heads, one board at a time: 1x1 convs (2 per policy role + 1 value) from the fp32
-    // residual registers, then the dense layers + softmaxes in fp32 -------------------------
+    // ---- the heads' 1x1 convs (2 per policy role + 1 value) from the fp32 residual registers;
+    // features in the model's Flatten order go to the scratch for heads_kernel ----------------
     const int HC = 2 * kp.R + 1;
     float* hpart = (float*)SCR;                                  // [4][HC][NPOS]
-    float* feat = (float*)(SCR + align16(4 * HC * NPOS * 4));    // [HC][NPOS] flattened per head
-    float* lg = (float*)((char*)feat + align16(HC * NPOS * 4));  // logits / hidden scratch
-    float* red = (float*)((char*)lg + align16((kp.maxP > kp.VH ? kp.maxP : kp.VH) * 4));
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
         const int board = board0 + bb;
-        const bool live = board < kp.n;
-        const int sg = find_segment(kp, board);
-        const int row = board - kp.seg[sg].row0;
         for (int h = 0; h < HC; ++h) {
             float wv[CT][4];
 #pragma unroll
@@ -460,73 +488,138 @@ forward_kernel(const KParams kp) {
             }
         }
         __syncthreads();
-        for (int i = tid; i < HC * NPOS; i += kThreads) {
-            const int h = i / NPOS, p = i - (i / NPOS) * NPOS;
-            float s = kp.bh[h];
+        if (board < kp.n) {
+            float* fo = kp.feat + (size_t)board * HC * NPOS;
+            for (int i = tid; i < HC * NPOS; i += kThreads) {
+                const int h = i / NPOS, p = i - (i / NPOS) * NPOS;
+                float s = kp.bh[h];
 #pragma unroll
-            for (int w = 0; w < 4; ++w) s += hpart[(w * HC + h) * NPOS + p];
-            s = act_fn(s, kp.leaky);
-            if (h < 2 * kp.R) {
-                const int r = h >> 1, c = h & 1;
-                const int idx = kp.flatten_nchw ? c * NPOS + p : p * 2 + c;
-                feat[r * 2 * NPOS + idx] = s;
-            } else {
-                feat[2 * kp.R * NPOS + p] = s;
+                for (int w = 0; w < 4; ++w) s += hpart[(w * HC + h) * NPOS + p];
+                s = act_fn(s, kp.leaky);
+                if (h < 2 * kp.R) {
+                    const int r = h >> 1, c = h & 1;
+                    const int idx = kp.flatten_nchw ? c * NPOS + p : p * 2 + c;
+                    fo[r * 2 * NPOS + idx] = s;
+                } else {
+                    fo[2 * kp.R * NPOS + p] = s;
+                }
             }
         }
-        __syncthreads();
-        if (bb == 0) GZ_STAMP(3);
-
-        // policy heads: Dense(2HW -> P_r) + softmax
-        for (int r = 0; r < kp.R; ++r) {
-            const int P = kp.P[r];
-            const float* pf = feat + r * 2 * NPOS;
-            const float* wd = kp.pd[r];
-            dense_rows<2 * NPOS, 4>(wd, kp.pb[r], P, pf, lg, wave, lane);
-            __syncthreads();
-            float lmax = -3.0e38f;
-            for (int j = tid; j < P; j += kThreads) lmax = fmaxf(lmax, lg[j]);
-            const float m = block_reduce<true, 4>(lmax, red);
-            float lsum = 0.f;
-            for (int j = tid; j < P; j += kThreads) {
-                const float e = __expf(lg[j] - m);
-                lg[j] = e;
-                lsum += e;
-            }
-            const float ssum = block_reduce<false, 4>(lsum, red);
-            const float inv = 1.f / ssum;
-            if (live) {
-                float* out = kp.seg[sg].pol[r] + (size_t)row * P;
-                for (int j = tid; j < P; j += kThreads) out[j] = lg[j] * inv;
-            }
-            __syncthreads();
-        }
-
-        if (bb == 0) GZ_STAMP(4);
-        // value head: Dense(HW -> VH) + act, Dense(VH -> V) + softmax
-        const float* vf = feat + 2 * kp.R * NPOS;
-        dense_rows<NPOS, 4>(kp.vhw, kp.vhb, kp.VH, vf, lg, wave, lane);
-        __syncthreads();
-        for (int k = tid; k < kp.VH; k += kThreads) lg[k] = act_fn(lg[k], kp.leaky);
-        __syncthreads();
-        if (wave < kp.V) {
-            float s = 0.f;
-            for (int k = lane; k < kp.VH; k += 64) s += lg[k] * kp.vdw[(size_t)k * kp.V + wave];
-            s = wave_sum(s);
-            if (lane == 0) red[16 + wave] = s + kp.vdb[wave];
-        }
-        __syncthreads();
-        if (tid == 0 && live) {
-            float m = red[16];
-            for (int v = 1; v < kp.V; ++v) m = fmaxf(m, red[16 + v]);
-            float e[4], sum = 0.f;
-            for (int v = 0; v < kp.V; ++v) { e[v] = __expf(red[16 + v] - m); sum += e[v]; }
-            for (int v = 0; v < kp.V; ++v) kp.seg[sg].val[(size_t)row * kp.V + v] = e[v] / sum;
-        }
-        __syncthreads();    // scratch is reused by the next board
+        __syncthreads();    // hpart is reused by the next board
     }
-    GZ_STAMP(5);
+    GZ_STAMP(3);
 #undef GZ_STAMP
+}
+
+// ---- heads -------------------------------------------------------------------------------------
+// kHeadBoards boards per workgroup of 4 waves.  Dense layers in fp32: thread j owns output j (of
+// P_r or VH) for every board of the workgroup; the k-major weights are read coalesced, each once
+// per workgroup, and the features come from LDS as one broadcast float4 per k (k-major, board-minor
+// image).  Each board's sums run in a fixed k order: outputs are independent of batch composition.
+__global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
+    constexpr int BPW = kHeadBoards;
+    static_assert(BPW == 4, "one float4 of features per k, one softmax wave per board");
+    extern __shared__ __attribute__((aligned(16))) float hs[];
+    const int NPOS = kp.npos, HC = 2 * kp.R + 1, FS = HC * NPOS;
+    const int LMAX = kp.maxP > kp.VH ? kp.maxP : kp.VH;
+    float* fk = hs;                       // [FS][BPW]
+    float* lg = hs + FS * BPW;            // [BPW][LMAX]
+    float* red = lg + BPW * LMAX;         // [BPW][4]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int board0 = blockIdx.x * BPW;
+    const int nb = kp.n - board0 < BPW ? kp.n - board0 : BPW;
+
+    for (int i = tid; i < BPW * FS; i += 256) {
+        const int b = i / FS, k = i - b * FS;
+        fk[k * BPW + b] = b < nb ? kp.feat[(size_t)(board0 + b) * FS + k] : 0.f;
+    }
+    __syncthreads();
+
+    // policy heads: Dense(2HW -> P_r) + softmax
+    for (int r = 0; r < kp.R; ++r) {
+        const int P = kp.P[r], K = 2 * NPOS;
+        const float* Wd = kp.pd[r];
+        const float4* f4 = (const float4*)(fk + (size_t)r * 2 * NPOS * BPW);
+        for (int j = tid; j < P; j += 256) {
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll 8
+            for (int k = 0; k < K; ++k) {
+                const float w = Wd[(size_t)k * P + j];
+                const float4 f = f4[k];
+                a0 += f.x * w; a1 += f.y * w; a2 += f.z * w; a3 += f.w * w;
+            }
+            const float bj = kp.pb[r][j];
+            lg[0 * LMAX + j] = a0 + bj;
+            lg[1 * LMAX + j] = a1 + bj;
+            lg[2 * LMAX + j] = a2 + bj;
+            lg[3 * LMAX + j] = a3 + bj;
+        }
+        __syncthreads();
+        if (wave < nb) {                  // wave b: softmax of board b
+            const int b = wave;
+            const float* l = lg + b * LMAX;
+            float m = -3.0e38f;
+            for (int j = lane; j < P; j += 64) m = fmaxf(m, l[j]);
+            m = wave_max(m);
+            float s = 0.f;
+            for (int j = lane; j < P; j += 64) s += __expf(l[j] - m);
+            s = wave_sum(s);
+            const float inv = 1.f / s;
+            const int board = board0 + b;
+            const int sg = find_segment(kp, board);
+            float* out = kp.seg[sg].pol[r] + (size_t)(board - kp.seg[sg].row0) * P;
+            for (int j = lane; j < P; j += 64) out[j] = __expf(l[j] - m) * inv;
+        }
+        __syncthreads();
+    }
+
+    // value head: Dense(HW -> VH) + act, Dense(VH -> V) + softmax
+    {
+        const int VH = kp.VH;
+        const float4* f4 = (const float4*)(fk + (size_t)2 * kp.R * NPOS * BPW);
+        for (int j = tid; j < VH; j += 256) {
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll 8
+            for (int k = 0; k < NPOS; ++k) {
+                const float w = kp.vhw[(size_t)k * VH + j];
+                const float4 f = f4[k];
+                a0 += f.x * w; a1 += f.y * w; a2 += f.z * w; a3 += f.w * w;
+            }
+            const float bj = kp.vhb[j];
+            lg[0 * LMAX + j] = act_fn(a0 + bj, kp.leaky);
+            lg[1 * LMAX + j] = act_fn(a1 + bj, kp.leaky);
+            lg[2 * LMAX + j] = act_fn(a2 + bj, kp.leaky);
+            lg[3 * LMAX + j] = act_fn(a3 + bj, kp.leaky);
+        }
+        __syncthreads();
+        if (wave < nb) {
+            const int b = wave;
+            const float* hv = lg + b * LMAX;
+            float o[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int v = 0; v < kp.V; ++v) {
+                float s = 0.f;
+                for (int k = lane; k < VH; k += 64) s += hv[k] * kp.vdw[(size_t)k * kp.V + v];
+                o[v] = wave_sum(s) + kp.vdb[v];
+            }
+            if (lane == 0) {
+                float m = o[0];
+                for (int v = 1; v < kp.V; ++v) m = fmaxf(m, o[v]);
+                float e[4], sum = 0.f;
+                for (int v = 0; v < kp.V; ++v) { e[v] = __expf(o[v] - m); sum += e[v]; }
+                const int board = board0 + b;
+                const int sg = find_segment(kp, board);
+                float* out = kp.seg[sg].val + (size_t)(board - kp.seg[sg].row0) * kp.V;
+                for (int v = 0; v < kp.V; ++v) out[v] = e[v] / sum;
+            }
+        }
+    }
+    (void)red;
+}
+
+__host__ inline int heads_lds_bytes(int npos, int R, int maxP, int VH) {
+    const int FS = (2 * R + 1) * npos;
+    const int LMAX = maxP > VH ? maxP : VH;
+    return (FS * kHeadBoards + kHeadBoards * LMAX + kHeadBoards * 4) * 4;
 }
 
 }  // namespace gznn

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -36,9 +38,13 @@ struct gz_net {
     int device = 0;
     int K0 = 0;
     size_t nweights = 0;
-    int smem = 0;
-    const void* kfn = nullptr;
-    int nb = 1;                    // boards per workgroup of the selected kernel variant
+    struct Trunk {
+        const void* fn = nullptr;
+        int nb = 1;                // boards per workgroup
+        int smem = 0;              // dynamic LDS bytes
+        int btab_off = 0;          // LDS offset of the bias table
+    } small, large;                // launches below / from large_min_rows rows
+    int large_min_rows = 1 << 30;
     bool has_weights = false;
 
     char* dmem = nullptr;          // all weights, one allocation
@@ -49,6 +55,9 @@ struct gz_net {
     float* d_io = nullptr;         // staging: planes + outputs
     int io_cap = 0;
     float last_ms = 0.f;
+    int heads_smem = 0;
+    std::mutex feat_mu;            // head-feature scratch, one per stream (launches on one stream are ordered)
+    std::map<hipStream_t, std::pair<float*, int>> feat;
     unsigned long long* d_stamps = nullptr;   // GZ_KERNEL_STAMPS diagnostics
     int stamp_cap = 0;
     bool stamps_on = false;
@@ -71,7 +80,7 @@ struct KernelChoice {
 template <int F, int H, int W, int NB, int WPE>
 static KernelChoice kernel_for() {
     KernelChoice k;
-    k.fn = (const void*)&forward_kernel<F, H, W, NB, WPE>;
+    k.fn = (const void*)&trunk_kernel<F, H, W, NB, WPE>;
     k.act_bytes = Geo<F, H, W, NB>::ACT_BYTES;
     k.nb = NB;
     return k;
@@ -82,25 +91,19 @@ static KernelChoice variants(int v) {
     switch (v) {
         case 11: return kernel_for<F, H, W, 1, 1>();
         case 12: return kernel_for<F, H, W, 1, 2>();
-        case 13: return kernel_for<F, H, W, 1, 3>();
-        case 14: return kernel_for<F, H, W, 1, 4>();
         case 21: return kernel_for<F, H, W, 2, 1>();
-        case 22: return kernel_for<F, H, W, 2, 2>();
-        case 41: return kernel_for<F, H, W, 4, 1>();
         default: return KernelChoice{};
     }
 }
 
-static int default_variant(int F, int H, int W) {
-    // measured on MI355X (profiles/r01_kernel_variants.txt): 3 workgroups/CU wins on 128x8x8,
-    // 2 elsewhere; 2 boards per workgroup only pays at batches >= 1024
-    if (F == 128 && H == 8 && W == 8) return 13;
-    return 12;
-}
+// Measured on MI355X (profiles/r01c_kernel_variants.txt): one board per workgroup with the whole
+// register file (11) is fastest while the launch has fewer boards than ~1.5x the CU count; from
+// there two boards per workgroup (21) win, each weight fragment feeding twice the MFMAs.  Every
+// variant computes each row identically (tests/test_nn_gpu.py::test_kernel_variants_identical), so
+// choosing per launch keeps results batch-invariant.
+constexpr int kSmallVariant = 11, kLargeVariant = 21, kLargeMinRows = 384;
 
-static KernelChoice select_kernel(int F, int H, int W) {
-    int v = default_variant(F, H, W);
-    if (const char* e = getenv("GZ_KERNEL_VARIANT")) v = atoi(e);
+static KernelChoice select_kernel(int F, int H, int W, int v) {
 #define GZ_CASE(F_, H_, W_) \
     if (F == F_ && H == H_ && W == W_) return variants<F_, H_, W_>(v);
     GZ_CASE(64, 6, 6)
@@ -136,9 +139,14 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     if (d.cnn_kernel_size != 3) { fail("only cnn_kernel_size 3 is supported"); return nullptr; }
     if (d.role_count < 1 || d.role_count > GZ_MAX_ROLES) { fail("role_count out of range"); return nullptr; }
     if (d.num_values < 1 || d.num_values > 4) { fail("num_values out of range"); return nullptr; }
-    const KernelChoice kc = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows);
-    const void* k = kc.fn;
-    if (!k) {
+    int vs = kSmallVariant, vl = kLargeVariant, min_large = kLargeMinRows;
+    if (const char* e = getenv("GZ_KERNEL_VARIANT")) {   // experiments: one fixed variant
+        vs = vl = atoi(e);
+        min_large = 1 << 30;
+    }
+    const KernelChoice kc = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vs);
+    const KernelChoice kl = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vl);
+    if (!kc.fn || !kl.fn) {
         fail("unsupported network geometry F=" + std::to_string(d.cnn_filter_size) + " H=" +
              std::to_string(d.input_columns) + " W=" + std::to_string(d.input_rows));
         return nullptr;
@@ -146,8 +154,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     gz_net* net = new gz_net;
     net->d = d;
     net->device = device;
-    net->kfn = k;
-    net->nb = kc.nb;
+    net->large_min_rows = min_large;
     net->K0 = ((9 * d.input_channels + 31) / 32) * 32;
     net->nweights = spec_count(d);
     int maxP = 0;
@@ -155,8 +162,18 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     const int npos = d.input_columns * d.input_rows;
     // LDS: two ping-pong activation images per board; the scratch (input staging, heads) aliases
     // the second image set, which holds nothing live at those times.
-    const int scr = scratch_bytes(npos, d.input_channels, net->K0, d.role_count, maxP, d.value_hidden_size);
-    net->smem = kc.nb * kc.act_bytes + std::max(kc.nb * kc.act_bytes, scr);
+    const int scr = trunk_scratch_bytes(npos, d.input_channels, net->K0, d.role_count);
+    auto trunk = [&](const KernelChoice& c) {
+        gz_net::Trunk t;
+        t.fn = c.fn;
+        t.nb = c.nb;
+        t.btab_off = c.nb * c.act_bytes + std::max(c.nb * c.act_bytes, scr);
+        t.smem = t.btab_off + bias_table_bytes(d.cnn_filter_size, d.residual_layers);
+        return t;
+    };
+    net->small = trunk(kc);
+    net->large = trunk(kl);
+    net->heads_smem = heads_lds_bytes(npos, d.role_count, maxP, d.value_hidden_size);
     KParams& kp = net->kp;
     kp.C = d.input_channels;
     kp.K0 = net->K0;
@@ -167,6 +184,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     kp.leaky = d.leaky_relu;
     kp.flatten_nchw = d.flatten_nchw;
     kp.maxP = maxP;
+    kp.npos = npos;
     for (int r = 0; r < d.role_count; ++r) kp.P[r] = d.policy_dist_count[r];
 
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&net->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -175,12 +193,20 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         delete net;
         return nullptr;
     }
-    if (net->smem > 64 * 1024) {
-        if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, net->smem) != hipSuccess) {
+    for (const gz_net::Trunk* t : {&net->small, &net->large}) {
+        if (t->smem > 64 * 1024 &&
+            hipFuncSetAttribute(t->fn, hipFuncAttributeMaxDynamicSharedMemorySize, t->smem) != hipSuccess) {
             fail("cannot raise dynamic LDS limit");
             delete net;
             return nullptr;
         }
+    }
+    if (net->heads_smem > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)&heads_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, net->heads_smem) !=
+            hipSuccess) {
+        fail("cannot raise dynamic LDS limit (heads)");
+        delete net;
+        return nullptr;
     }
     return net;
 }
@@ -191,6 +217,7 @@ extern "C" void gz_net_destroy(gz_net* net) {
     if (net->dmem) (void)hipFree(net->dmem);
     if (net->d_io) (void)hipFree(net->d_io);
     if (net->d_stamps) (void)hipFree(net->d_stamps);
+    for (auto& f : net->feat) (void)hipFree(f.second.first);
     if (net->ev0) (void)hipEventDestroy(net->ev0);
     if (net->ev1) (void)hipEventDestroy(net->ev1);
     if (net->stream) (void)hipStreamDestroy(net->stream);
@@ -321,21 +348,11 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     put(o_wh, wh.data(), wh.size() * 4);
     put(o_bh, bh.data(), bh.size() * 4);
     for (int r = 0; r < R; ++r) {
-        // transposed to [P_r][2HW]: one output row is contiguous for the row-parallel dense
-        const int P = d.policy_dist_count[r];
-        std::vector<float> t((size_t)P * 2 * HW);
-        for (int i = 0; i < 2 * HW; ++i)
-            for (int j = 0; j < P; ++j) t[(size_t)j * 2 * HW + i] = pdense[r][(size_t)i * P + j];
-        put(o_pd[r], t.data(), t.size() * 4);
+        // Keras layout [2HW][P_r] (k-major): heads_kernel reads one k row coalesced across outputs
+        put(o_pd[r], pdense[r], (size_t)2 * HW * d.policy_dist_count[r] * 4);
         put(o_pb[r], pbias[r], (size_t)d.policy_dist_count[r] * 4);
     }
-    {   // transposed to [VH][HW]
-        const int VH = d.value_hidden_size;
-        std::vector<float> t((size_t)VH * HW);
-        for (int p = 0; p < HW; ++p)
-            for (int k = 0; k < VH; ++k) t[(size_t)k * HW + p] = vhw[(size_t)p * VH + k];
-        put(o_vhw, t.data(), t.size() * 4);
-    }
+    put(o_vhw, vhw, (size_t)HW * d.value_hidden_size * 4);   // Keras layout [HW][VH]
     put(o_vhb, vhb, d.value_hidden_size * 4);
     put(o_vdw, vdw, (size_t)d.value_hidden_size * d.num_values * 4);
     put(o_vdb, vdb, d.num_values * 4);
@@ -373,7 +390,8 @@ extern "C" int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_
     return gz_net_set_weights(net, h.data(), count);
 }
 
-static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* segs, int nseg) {
+static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* segs, int nseg,
+                           hipEvent_t mid = nullptr) {
     if (!net->has_weights) return fail("weights not set");
     if (nseg < 1 || nseg > kMaxSegments) return fail("segment count out of range (1.." + std::to_string(kMaxSegments) + ")");
     KParams kp = net->kp;
@@ -391,8 +409,28 @@ static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* se
     kp.n = n;
     kp.nseg = nseg;
     kp.stamps = net->stamps_on ? net->d_stamps : nullptr;
+    {   // head-feature scratch of this stream (grown with a device sync: rare, sizes only increase)
+        std::lock_guard<std::mutex> lk(net->feat_mu);
+        auto& f = net->feat[stream];
+        if (f.second < n) {
+            if (f.first) {
+                HIPCHK(hipDeviceSynchronize());
+                HIPCHK(hipFree(f.first));
+                f.first = nullptr;
+            }
+            const int cap = std::max(n, 8192);
+            HIPCHK(hipMalloc((void**)&f.first, (size_t)cap * (2 * kp.R + 1) * kp.npos * sizeof(float)));
+            f.second = cap;
+        }
+        kp.feat = f.first;
+    }
+    const gz_net::Trunk& t = n >= net->large_min_rows ? net->large : net->small;
+    kp.btab_off = t.btab_off;
     void* args[] = {&kp};
-    HIPCHK(hipLaunchKernel(net->kfn, dim3((n + net->nb - 1) / net->nb), dim3(256), args, net->smem, stream));
+    HIPCHK(hipLaunchKernel(t.fn, dim3((n + t.nb - 1) / t.nb), dim3(256), args, t.smem, stream));
+    if (mid) HIPCHK(hipEventRecord(mid, stream));
+    HIPCHK(hipLaunchKernel((const void*)&heads_kernel, dim3((n + kHeadBoards - 1) / kHeadBoards), dim3(256), args,
+                           net->heads_smem, stream));
     return 0;
 }
 
@@ -418,6 +456,12 @@ extern "C" int gz_net_forward_segments(gz_net* net, void* stream, const gz_segme
     return launch_segments(net, (hipStream_t)stream, segs, nseg);
 }
 
+extern "C" int gz_net_forward_segments_ev(gz_net* net, void* stream, const gz_segment* segs, int nseg,
+                                          void* trunk_done_event) {
+    if (!net || !segs) return fail("null argument");
+    return launch_segments(net, (hipStream_t)stream, segs, nseg, (hipEvent_t)trunk_done_event);
+}
+
 extern "C" int gz_net_forward(gz_net* net, const float* planes, int n, float* const* policies, float* values) {
     if (!net || !planes || !policies || !values) return fail("null argument");
     if (n <= 0) return 0;
@@ -439,7 +483,7 @@ extern "C" int gz_net_forward(gz_net* net, const float* planes, int n, float* co
     float* d_val = p;
     HIPCHK(hipMemcpyAsync(d_in, planes, (size_t)n * in_f * 4, hipMemcpyHostToDevice, net->stream));
     const bool stamps = getenv("GZ_KERNEL_STAMPS") != nullptr;
-    const int grid = (n + net->nb - 1) / net->nb;
+    const int grid = n;   // >= workgroups of either trunk variant
     if (stamps && grid > net->stamp_cap) {
         if (net->d_stamps) HIPCHK(hipFree(net->d_stamps));
         HIPCHK(hipMalloc((void**)&net->d_stamps, (size_t)grid * 8 * sizeof(unsigned long long)));
@@ -461,7 +505,7 @@ extern "C" int gz_net_forward(gz_net* net, const float* planes, int n, float* co
         HIPCHK(hipMemcpy(h.data(), net->d_stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         for (int i = 0; i < 8; ++i) net->stamp_avg[i] = 0;
         for (int b = 0; b < grid; ++b)
-            for (int i = 1; i < 6; ++i) net->stamp_avg[i] += (double)(h[(size_t)b * 8 + i] - h[(size_t)b * 8 + i - 1]) / grid;
+            for (int i = 1; i < 4; ++i) net->stamp_avg[i] += (double)(h[(size_t)b * 8 + i] - h[(size_t)b * 8 + i - 1]) / grid;
     }
     return 0;
 }

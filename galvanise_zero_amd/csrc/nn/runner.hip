@@ -45,7 +45,7 @@ struct Pool {
 };
 
 struct Batch {
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;
     std::vector<int> pools;
     int rows = 0;
 };
@@ -74,7 +74,7 @@ struct gz_runner {
 
     std::atomic<bool> stop{false};
     std::atomic<long> batches{0}, rows{0}, launches{0}, samples_taken{0}, segments{0};
-    std::atomic<long> kernel_us{0};
+    std::atomic<long> kernel_us{0}, trunk_us{0};
     std::mutex m;
     std::condition_variable cv;
     std::atomic<int> failed{0};
@@ -170,6 +170,8 @@ static void launcher_main(gz_runner* r) {
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, b.ev0, b.ev1) == hipSuccess)
                 r->kernel_us.fetch_add((long)(ms * 1000.0f), std::memory_order_relaxed);
+            if (hipEventElapsedTime(&ms, b.ev0, b.evm) == hipSuccess)
+                r->trunk_us.fetch_add((long)(ms * 1000.0f), std::memory_order_relaxed);
             for (int i : b.pools) {
                 Pool& p = r->pools[i];
                 p.rows_done = p.rows;
@@ -220,7 +222,7 @@ static void launcher_main(gz_runner* r) {
             segs[k].values = p.h_val;
         }
         if (hipEventRecord(b.ev0, r->stream) != hipSuccess ||
-            gz_net_forward_segments(r->net, r->stream, segs.data(), (int)segs.size()) != 0 ||
+            gz_net_forward_segments_ev(r->net, r->stream, segs.data(), (int)segs.size(), b.evm) != 0 ||
             hipEventRecord(b.ev1, r->stream) != hipSuccess) {
             set_failed(r, std::string("launch failed: ") + gz_nn_last_error());
             return;
@@ -274,7 +276,8 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
     r->policy_sizes.assign(policy_sizes, policy_sizes + num_policies);
     bool ok = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess;
     for (Batch& b : r->batches_ring)
-        ok = ok && hipEventCreate(&b.ev0) == hipSuccess && hipEventCreate(&b.ev1) == hipSuccess;
+        ok = ok && hipEventCreate(&b.ev0) == hipSuccess && hipEventCreate(&b.evm) == hipSuccess &&
+             hipEventCreate(&b.ev1) == hipSuccess;
     if (!ok) {
         g_err = "stream / event creation failed";
         gz_runner_destroy(r);
@@ -361,6 +364,7 @@ extern "C" int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out) {
     out->batches = r->batches.load();
     out->rows = r->rows.load();
     out->kernel_ms = r->kernel_us.load() / 1000.0;
+    out->trunk_ms = r->trunk_us.load() / 1000.0;
     out->kernel_launches = r->launches.load();
     out->samples = r->samples_taken.load();
     out->segments = r->segments.load();
@@ -405,6 +409,7 @@ extern "C" void gz_runner_destroy(gz_runner* r) {
     for (Batch& b : r->batches_ring) {
         if (b.ev0) (void)hipEventDestroy(b.ev0);
         if (b.ev1) (void)hipEventDestroy(b.ev1);
+        if (b.evm) (void)hipEventDestroy(b.evm);
     }
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;

@@ -62,6 +62,17 @@ class NetDesc:
         return f
 
 
+    def flops_trunk(self):
+        """FLOPs of the trunk kernel per evaluation: every conv incl. the heads' 1x1 convs."""
+        F, C, HW, k = self.cnn_filter_size, self.input_channels, self.hw, self.cnn_kernel_size
+        f = 2 * HW * C * F * k * k + self.residual_layers * 2 * (2 * HW * F * F * k * k)
+        return f + (2 * self.role_count + 1) * 2 * HW * F
+
+    def flops_heads(self):
+        """FLOPs of the heads kernel per evaluation: the dense layers."""
+        return self.flops_per_eval() - self.flops_trunk()
+
+
 def weight_spec(d: NetDesc) -> List[Tuple[str, Tuple[int, ...]]]:
     """Ordered (name, shape) list of the canonical float32 weight blob."""
     F, C, k = d.cnn_filter_size, d.input_channels, d.cnn_kernel_size

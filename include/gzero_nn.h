@@ -64,8 +64,13 @@ typedef struct gz_segment {
     float* values;                            /* [rows][num_values] */
 } gz_segment;
 
-/* Asynchronous forward of up to GZ_MAX_SEGMENTS segments as ONE kernel launch on `stream`. */
+/* Asynchronous forward of up to GZ_MAX_SEGMENTS segments on `stream`: one trunk launch (planes ->
+ * head features) and one heads launch (features -> policies / values) for all segments. */
 int gz_net_forward_segments(gz_net* net, void* stream, const gz_segment* segs, int nseg);
+/* Same, recording `trunk_done_event` (a hipEvent_t, may be NULL) between the two launches so the
+ * caller can time the trunk kernel alone. */
+int gz_net_forward_segments_ev(gz_net* net, void* stream, const gz_segment* segs, int nseg,
+                               void* trunk_done_event);
 
 /* Synchronous forward, host buffers: planes float32 [n][C][H][W] (the poll() buffer layout,
  * cppinterface.py:114); policies[r] float32 [n][P_r]; values float32 [n][num_values].
@@ -77,7 +82,7 @@ int gz_net_forward(gz_net* net, const float* planes, int n,
 int gz_net_forward_device(gz_net* net, void* stream, const float* d_planes, int n,
                           float* const* d_policies, float* d_values);
 
-/* Device time (ms) of the last gz_net_forward kernel, measured with HIP events on its stream. */
+/* Device time (ms) of the last gz_net_forward (both launches), measured with HIP events on its stream. */
 float gz_net_last_kernel_ms(const gz_net* net);
 
 /* Algorithmic FLOPs of one leaf evaluation (2 FLOP/MAC). */
@@ -118,7 +123,8 @@ typedef struct gz_runner_config {
 typedef struct gz_runner_stats {
     long batches;                /* NN forwards completed */
     long rows;                   /* leaf evaluations completed */
-    double kernel_ms;            /* summed forward-kernel device time (HIP events around each launch) */
+    double kernel_ms;            /* summed forward device time (HIP events around trunk + heads launches) */
+    double trunk_ms;             /* summed trunk-kernel device time (events around the trunk launch) */
     long kernel_launches;
     long games_completed;
     long games_with_samples;

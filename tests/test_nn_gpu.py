@@ -95,3 +95,17 @@ def test_large_batch_and_timing(hip_device):
     tflops = desc.flops_per_eval() * 1024 / (ms * 1e-3) / 1e12
     print("cfg2 N=1024 kernel %.3f ms  %.1f TFLOP/s" % (ms, tflops))
     assert ms > 0
+
+
+@pytest.mark.parametrize("variant", ["11", "12", "21"])
+def test_kernel_variants_identical(variant, hip_device, monkeypatch):
+    """Every compiled trunk variant (boards per workgroup x workgroups per CU) computes each row
+    with the same operations in the same order: outputs are bit-identical to the default's."""
+    desc = VARIANTS["cfg2"]
+    x = random_planes(desc, 33, 4)
+    net, _ = _net(desc, 5, hip_device)
+    base = net.forward(x)
+    monkeypatch.setenv("GZ_KERNEL_VARIANT", variant)
+    vnet, _ = _net(desc, 5, hip_device)
+    for a, b in zip(base, vnet.forward(x)):
+        assert np.array_equal(a, b)

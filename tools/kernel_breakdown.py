@@ -54,8 +54,8 @@ def main():
             st = net.stamp_avg()
             net.close()
             del os.environ["GZ_KERNEL_STAMPS"]
-            print("variant %s N=%d stamps (cycles per workgroup): input+conv0 %.0f, trunk %.0f, head 1x1 %.0f, "
-                  "policy %.0f, value %.0f" % ((v, n) + tuple(st[1:6])), flush=True)
+            print("variant %s N=%d trunk-kernel stamps (cycles per workgroup): input+conv0 %.0f, residual trunk %.0f, "
+                  "head 1x1 convs + features %.0f" % ((v, n) + tuple(st[1:4])), flush=True)
             slope, icpt = np.polyfit(xs, ys, 1)
             conv_flops = 2 * 64 * 128 * 128 * 9 * 2 * n
             print("variant %s N=%d: %.1f us per residual block (%.0f TFLOP/s in the trunk), %.1f us fixed"

@@ -18,7 +18,7 @@ from galvanise_zero_amd._native import HipNet  # noqa: E402
 from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS  # noqa: E402
 from galvanise_zero_amd.nn.weights import random_planes, random_weights, to_blob  # noqa: E402
 
-VARIANTS = ["12", "11", "13", "14", "21", "22", "41"]
+VARIANTS = ["default", "12", "11", "21"]
 
 
 def main():
@@ -35,7 +35,10 @@ def main():
         xs = {n: random_planes(desc, n, 5 + n) for n in batches}
         base = {}
         for v in args.variants.split(","):
-            os.environ["GZ_KERNEL_VARIANT"] = v
+            if v == "default":        # the library's per-launch dispatch
+                os.environ.pop("GZ_KERNEL_VARIANT", None)
+            else:
+                os.environ["GZ_KERNEL_VARIANT"] = v
             try:
                 net = HipNet(desc, 0)
             except RuntimeError as e:

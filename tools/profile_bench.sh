@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 passes for the round's profile evidence (run on the GPU box from the repo root):
-#   1. FETCH_SIZE and WRITE_SIZE (separate passes: TCC slots) and SQ counters on the NN forward
-#      alone at the bench's eval batch (tools/kernel_variants.py, default variant)
+#   1. FETCH_SIZE, WRITE_SIZE (separate passes: TCC slots) and SQ counters on the forward alone at
+#      the bench's typical launch size (tools/kernel_variants.py, 512 rows, default dispatch)
 #   2. kernel trace + stats of a short bench run (per-kernel average duration)
 # Usage: tools/profile_bench.sh <tag> [bench args...]
 set -o pipefail
@@ -10,7 +10,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-KV="$R/tools/kernel_variants.py --configs 2 --batches 256 --reps 30 --variants 13"
+KV="$R/tools/kernel_variants.py --configs 2 --batches 512 --reps 30 --variants default"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 $KV \
     > $OUT/fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 $KV \
