@@ -356,10 +356,28 @@ bool PuctEvaluator::convergedFast(int count, bool* out) const {
     return true;
 }
 
-// Unsorted selection; returns false when the literal sorted loop must run instead.
+// comparator of sortedChildrenSelect (evaluator.cpp:242-263)
+static inline bool selectBefore(const PuctNodeChild* a, const PuctNodeChild* b, int lead) {
+    const float sa = a->to_node == nullptr ? -1 : a->to_node->getCurrentScore(lead);
+    const float sb = b->to_node == nullptr ? -1 : b->to_node->getCurrentScore(lead);
+    if (sa < 0 && sb < 0) return a->policy_prob_orig > b->policy_prob_orig;
+    return sa > sb;
+}
+
+// Unsorted selection; returns false when the literal sorted loop must run instead (the RNG is then
+// left exactly as it was on entry).
+//
+// Root latch (evaluator.cpp:461-475): at the root with 1000 < visits < 4e7 the reference draws
+// rng.get() once for every child that reaches the latch test, in sortedChildrenSelect order, and a
+// child is skipped when its draw is > 0.1 and its traversals exceed 16 and 0.66 * visits.  At most
+// one child d can exceed 0.66 * visits (traversals sum to at most visits), so only d's draw matters:
+// its position in the sorted order is the number of reaching children that sort strictly before it,
+// which is order-independent unless another reaching child ties with d under the comparator (then
+// the literal path runs).  The draws are made in the same number, d's is the one at that position.
 bool PuctEvaluator::selectChildFast(PuctNode* node, int depth, float prior_score, double sqrt_node_visits,
                                     PuctNodeChild** out) {
-    if (node->visits > 1000 && node->visits < 40000000 && depth == 0) return false;   // root latch draws RNG
+    const bool latch = node->visits > 1000 && node->visits < 40000000 && depth == 0;
+    const float limit_latch_root = 0.66;
     const int n = node->num_children;
     if (n > 512) return false;
     double scores[512];
@@ -369,6 +387,7 @@ bool PuctEvaluator::selectChildFast(PuctNode* node, int depth, float prior_score
     float win_key = 0.f;
     int best = -1;
     double best_score = 0.0;
+    int latch_d = -1, reach = 0;
     PuctNodeChild* cs = node->children();
     for (int i = 0; i < n; ++i) {
         PuctNodeChild* c = cs + i;
@@ -408,6 +427,11 @@ bool PuctEvaluator::selectChildFast(PuctNode* node, int depth, float prior_score
         }
         const double score = child_score + exploration_score;
         scores[i] = score;
+        ++reach;
+        if (latch && c->traversals > 16 && c->traversals > node->visits * limit_latch_root) {
+            if (latch_d >= 0) return false;
+            latch_d = i;
+        }
         if (best < 0 || score > best_score) {
             best = i;
             best_score = score;
@@ -419,13 +443,49 @@ bool PuctEvaluator::selectChildFast(PuctNode* node, int depth, float prior_score
         return true;
     }
     if (best < 0 || !(best_score > -1.0)) return false;
+    Rng saved_rng = rng;
+    if (latch) {
+        int rank = 0;
+        if (latch_d >= 0) {
+            if (reach < 2) return false;   // d alone: the fallback rules decide
+            const PuctNodeChild* d = cs + latch_d;
+            for (int i = 0; i < n; ++i) {
+                if (i == latch_d || scores[i] == -1e300) continue;
+                if (selectBefore(cs + i, d, lead)) ++rank;
+                else if (!selectBefore(d, cs + i, lead)) return false;   // tie: position undetermined
+            }
+        }
+        bool latched = false;
+        for (int j = 0; j < reach; ++j) {
+            const double v = rng.get();
+            if (j == rank && latch_d >= 0 && v > 0.1) latched = true;
+        }
+        if (latched) {
+            scores[latch_d] = -1e300;
+            best = -1;
+            for (int i = 0; i < n; ++i) {
+                if (scores[i] == -1e300) continue;
+                if (best < 0 || scores[i] > best_score) {
+                    best = i;
+                    best_score = scores[i];
+                }
+            }
+            if (best < 0 || !(best_score > -1.0)) {
+                rng = saved_rng;
+                return false;
+            }
+        }
+    }
     // order independence of `if (score > best_score_float)`: the max m must replace any incumbent
     // (m > float(c)) and never be replaced (c <= float(m)).
     const double fm = (float)best_score;
     for (int i = 0; i < n; ++i) {
         if (i == best || scores[i] == -1e300) continue;
         const double sc = scores[i];
-        if (sc > fm || !(best_score > (double)(float)sc)) return false;
+        if (sc > fm || !(best_score > (double)(float)sc)) {
+            rng = saved_rng;
+            return false;
+        }
     }
     *out = cs + best;
     return true;
@@ -449,11 +509,26 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
     const double sqrt_node_visits = std::sqrt(node->visits + 1);
 
     PuctNodeChild* fast_choice = nullptr;
+    const Rng rng_before = rng;
     const bool fast_ok = selectChildFast(node, depth, prior_score, sqrt_node_visits, &fast_choice);
     if (fast_ok && !verify_fastpath()) {
         path.emplace_back(node, fast_choice, fast_choice);
         return fast_choice;
     }
+    // verification: replay the literal loop from the same RNG state; it must end in the same state
+    const Rng rng_after_fast = rng;
+    rng = rng_before;
+    struct RngCheck {
+        const Rng& fast_state;
+        const Rng& live;
+        bool active;
+        ~RngCheck() {
+            if (active && !(fast_state == live)) {
+                std::fprintf(stderr, "gz fast-path selectChild RNG mismatch\n");
+                std::abort();
+            }
+        }
+    } rng_check{rng_after_fast, rng, fast_ok};
 
     float best_score = -1;
     PuctNodeChild* best_child = nullptr;

@@ -8,10 +8,13 @@
 
 namespace gz {
 
+static_assert(sizeof(PuctNode) == 64, "node header must be one cache line");
+
 static size_t node_bytes(int num_children, int role_count, int num_words) {
-    size_t n = sizeof(PuctNode) + sizeof(PuctNodeChild) * num_children + sizeof(Score) * 2 * role_count;
+    size_t n = sizeof(PuctNode) + sizeof(PuctNodeChild) * num_children + sizeof(Score) * role_count;
     n = (n + 7) & ~size_t(7);
-    return n + sizeof(uint64_t) * num_words;
+    n += sizeof(uint64_t) * num_words;
+    return (n + 63) & ~size_t(63);   // aligned_alloc: size is a multiple of the alignment
 }
 
 // node.cpp:111-149: children = cross product of every role's legal moves, role 0 outermost.
@@ -70,7 +73,7 @@ PuctNode* PuctNode::create(const uint64_t* base_state, StateMachine* sm) {
     }
 
     const size_t bytes = node_bytes(total_children, role_count, num_words);
-    PuctNode* node = static_cast<PuctNode*>(std::malloc(bytes));
+    PuctNode* node = static_cast<PuctNode*>(std::aligned_alloc(64, bytes));
     node->parent = nullptr;
     node->visits = 0;
     node->inflight_visits = 0;

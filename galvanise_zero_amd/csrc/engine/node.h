@@ -50,8 +50,12 @@ struct PuctNode {
     uint8_t role_count;
     uint16_t num_words;
     uint32_t allocated_size;
+    // Current scores live in the header: together with visits / is_finalised / unselectable_count
+    // they are all a parent's selection passes read of a child node, and the header is one 64-byte
+    // line (nodes are 64-byte aligned), so each child costs one cache line, not two.
+    Score current[kMaxRoles];
 
-    // trailing storage: children[num_children] | current[R] | final[R] | basestate words
+    // trailing storage: children[num_children] | final[R] | basestate words
     PuctNodeChild* children() { return reinterpret_cast<PuctNodeChild*>(this + 1); }
     const PuctNodeChild* children() const { return reinterpret_cast<const PuctNodeChild*>(this + 1); }
     PuctNodeChild* getNodeChild(int, int i) { return children() + i; }
@@ -60,14 +64,14 @@ struct PuctNode {
     Score* scoresPtr() { return reinterpret_cast<Score*>(children() + num_children); }
     const Score* scoresPtr() const { return reinterpret_cast<const Score*>(children() + num_children); }
 
-    Score getCurrentScore(int role) const { return scoresPtr()[role]; }
-    void setCurrentScore(int role, Score s) { scoresPtr()[role] = s; }
+    Score getCurrentScore(int role) const { return current[role]; }
+    void setCurrentScore(int role, Score s) { current[role] = s; }
     Score getFinalScore(int role, bool clamp = false) const {
-        Score s = scoresPtr()[role_count + role];
+        Score s = scoresPtr()[role];
         if (clamp) s = s < 0.0f ? 0.0f : (s > 1.0f ? 1.0f : s);
         return s;
     }
-    void setFinalScore(int role, Score s) { scoresPtr()[role_count + role] = s; }
+    void setFinalScore(int role, Score s) { scoresPtr()[role] = s; }
 
     uint64_t* getBaseState() { return reinterpret_cast<uint64_t*>(basestateOffset()); }
     const uint64_t* getBaseState() const { return reinterpret_cast<const uint64_t*>(basestateOffset()); }
@@ -87,7 +91,7 @@ struct PuctNode {
 
 private:
     char* basestateOffset() const {
-        uintptr_t p = reinterpret_cast<uintptr_t>(scoresPtr() + 2 * role_count);
+        uintptr_t p = reinterpret_cast<uintptr_t>(scoresPtr() + role_count);
         p = (p + 7) & ~uintptr_t(7);
         return reinterpret_cast<char*>(p);
     }

@@ -57,6 +57,8 @@ public:
 
     uint32_t getWithMax(uint32_t upper) { return upper ? (*this)() % upper : 0; }
 
+    bool operator==(const Rng& o) const { return s0 == o.s0 && s1 == o.s1; }
+
 private:
     static inline uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
     uint64_t s0, s1;

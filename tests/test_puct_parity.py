@@ -164,3 +164,13 @@ def test_spin_yield_keeps_each_game_identical(small):
         assert a[k][:n] == b[k][:n], k
     # the yields did change the batch composition (otherwise the test proves nothing)
     assert any(x.shape != y.shape or not np.array_equal(x, y) for x, y in zip(log_a, log_b))
+
+
+def test_player_root_latch_bit_exact():
+    """Past 1000 root visits the reference's root latch draws the RNG once per reaching child in
+    sorted order (evaluator.cpp:461-475); the engine's unsorted fast path must draw identically."""
+    setup = Setup("breakthroughSmall")
+    conf = templates.base_puct_config(batch_size=1, choose="choose_top_visits", dirichlet_noise_pct=0.25,
+                                      think_time=-1, converged_visits=1)
+    visits = _player_run(setup, conf, 1400, 2, seed=13)
+    assert sum(t for _, t, _ in visits[0]) > 1000
