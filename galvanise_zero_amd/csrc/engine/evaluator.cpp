@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <limits>
 #include <random>
 
@@ -146,18 +147,35 @@ PuctNode* PuctEvaluator::expandChild(PuctNode* parent, PuctNodeChild* child) {
 
 typedef std::vector<PuctNodeChild*> SortedChildren;
 
-// evaluator.cpp:242-263: by current score of the lead role desc; unexpanded (-1) by prior desc
+// evaluator.cpp:242-263: by current score of the lead role desc; unexpanded (-1) by prior desc.
+// The sort runs on compact by-value keys instead of child pointers: std::sort's permutation depends
+// only on the sequence of comparison results, which the keys reproduce exactly, and the keys avoid a
+// dereference of every child's node per comparison.
+struct SelectKey {
+    float s;        // current score of the lead role, -1 when unexpanded
+    float p;        // policy_prob_orig
+    PuctNodeChild* c;
+};
 static SortedChildren sortedChildrenSelect(PuctNode* node) {
-    SortedChildren children;
-    children.reserve(node->num_children);
-    for (int ii = 0; ii < node->num_children; ii++) children.push_back(node->getNodeChild(0, ii));
-    auto f = [node](const PuctNodeChild* a, const PuctNodeChild* b) {
-        const float sa = a->to_node == nullptr ? -1 : a->to_node->getCurrentScore(node->lead_role_index);
-        const float sb = b->to_node == nullptr ? -1 : b->to_node->getCurrentScore(node->lead_role_index);
-        if (sa < 0 && sb < 0) return a->policy_prob_orig > b->policy_prob_orig;
-        return sa > sb;
-    };
-    std::sort(children.begin(), children.end(), f);
+    const int n = node->num_children;
+    SelectKey stack_keys[128];
+    std::vector<SelectKey> heap_keys;
+    SelectKey* keys = stack_keys;
+    if (n > 128) {
+        heap_keys.resize(n);
+        keys = heap_keys.data();
+    }
+    for (int ii = 0; ii < n; ii++) {
+        PuctNodeChild* c = node->getNodeChild(0, ii);
+        keys[ii] = {c->to_node == nullptr ? -1 : c->to_node->getCurrentScore(node->lead_role_index),
+                    c->policy_prob_orig, c};
+    }
+    std::sort(keys, keys + n, [](const SelectKey& a, const SelectKey& b) {
+        if (a.s < 0 && b.s < 0) return a.p > b.p;
+        return a.s > b.s;
+    });
+    SortedChildren children(n);
+    for (int ii = 0; ii < n; ii++) children[ii] = keys[ii].c;
     return children;
 }
 
@@ -232,54 +250,20 @@ static inline bool visitsBefore(const PuctNodeChild* a, const PuctNodeChild* b) 
     return va > vb;
 }
 
-// Index of the unique first element under `before` among children with keep(i), or -1 if empty,
-// -2 if the first place is tied.
-template <typename Before, typename Keep>
-static int uniqueFirst(const PuctNode* node, Before before, Keep keep) {
-    int best = -1;
-    bool tied = false;
-    for (int i = 0; i < node->num_children; ++i) {
-        if (!keep(i)) continue;
-        const PuctNodeChild* c = node->getNodeChild(0, i);
-        if (best < 0) {
-            best = i;
-            continue;
-        }
-        const PuctNodeChild* b = node->getNodeChild(0, best);
-        if (before(c, b)) {
-            best = i;
-            tied = false;
-        } else if (!before(b, c)) {
-            tied = true;
-        }
-    }
-    return tied ? -2 : best;
-}
-
-// Second place (unique) after excluding `first`; -1 none, -2 tied (or not strictly after first).
-template <typename Before, typename Keep>
-static int uniqueSecond(const PuctNode* node, Before before, Keep keep, int first) {
-    const int s = uniqueFirst(node, before, [&](int i) { return i != first && keep(i); });
-    if (s >= 0 && !before(node->getNodeChild(0, first), node->getNodeChild(0, s))) return -2;
-    return s;
-}
-
-bool PuctEvaluator::chooseTopVisitsFast(const PuctNode* node, const PuctNodeChild** out) const {
-    // one pass: first win, first two non-losses and first overall under travBefore, with tie flags
-    const int ri = node->lead_role_index;
+// chooseTopVisits (evaluator.cpp:1100-1136) as one unsorted pass: first win, first two non-losses
+// and first overall under travBefore, with tie flags.  add() per child, then finish().
+struct TopVisitsScan {
     const PuctNodeChild *w = nullptr, *a = nullptr, *b = nullptr, *f = nullptr;
     bool w_tie = false, f_tie = false;
     int a_n = 0, b_n = 0;
-    const PuctNodeChild* cs = node->children();
-    for (int i = 0; i < node->num_children; ++i) {
-        const PuctNodeChild* c = cs + i;
+
+    __attribute__((always_inline)) inline void add(const PuctNodeChild* c, int ri) {
         bool win = false, loss = false;
         if (c->to_node != nullptr && c->to_node->is_finalised) {
             const Score sc = c->to_node->getCurrentScore(ri);
             win = sc > 0.99;
             loss = !win && sc < 0.01;
         }
-        // overall first
         if (f == nullptr || travBefore(c, f)) {
             f = c;
             f_tie = false;
@@ -295,7 +279,6 @@ bool PuctEvaluator::chooseTopVisitsFast(const PuctNode* node, const PuctNodeChil
             }
         }
         if (!loss) {
-            // top-2 with multiplicities: a (a_n equivalent elements), then b (b_n equivalent)
             if (a == nullptr) {
                 a = c;
                 a_n = 1;
@@ -314,39 +297,71 @@ bool PuctEvaluator::chooseTopVisitsFast(const PuctNode* node, const PuctNodeChil
             }
         }
     }
-    if (w != nullptr) {
-        if (w_tie) return false;
-        *out = w;
-        return true;
-    }
-    if (a_n > 1 || b_n > 1) return false;   // the first two non-loss places are not unique
-    if (conf->top_visits_best_guess_converge_ratio > 0 && a != nullptr && b != nullptr) {
-        if (a->to_node != nullptr && b->to_node != nullptr) {
-            if (b->traversals > a->traversals * conf->top_visits_best_guess_converge_ratio &&
-                b->to_node->getCurrentScore(ri) > a->to_node->getCurrentScore(ri))
-                *out = b;
-            else
-                *out = a;
+
+    // false: the sorted (exact) computation is needed
+    inline bool finish(int ri, float converge_ratio, const PuctNodeChild** out) const {
+        if (w != nullptr) {
+            if (w_tie) return false;
+            *out = w;
             return true;
         }
+        if (a_n > 1 || b_n > 1) return false;   // the first two non-loss places are not unique
+        if (converge_ratio > 0 && a != nullptr && b != nullptr) {
+            if (a->to_node != nullptr && b->to_node != nullptr) {
+                if (b->traversals > a->traversals * converge_ratio &&
+                    b->to_node->getCurrentScore(ri) > a->to_node->getCurrentScore(ri))
+                    *out = b;
+                else
+                    *out = a;
+                return true;
+            }
+        }
+        if (f == nullptr || f_tie) return false;
+        *out = f;
+        return true;
     }
-    if (f == nullptr || f_tie) return false;
-    *out = f;
-    return true;
+};
+
+bool PuctEvaluator::chooseTopVisitsFast(const PuctNode* node, const PuctNodeChild** out) const {
+    TopVisitsScan scan;
+    const PuctNodeChild* cs = node->children();
+    for (int i = 0; i < node->num_children; ++i) scan.add(cs + i, node->lead_role_index);
+    return scan.finish(node->lead_role_index, conf->top_visits_best_guess_converge_ratio, out);
 }
 
 bool PuctEvaluator::convergedFast(int count, bool* out) const {
-    if (root->num_children < 2) {
+    const int n = root->num_children;
+    if (n < 2) {
         *out = true;
         return true;
     }
-    auto all = [](int) { return true; };
-    const int i0 = uniqueFirst(root, visitsBefore, all);
-    if (i0 < 0) return false;
-    const int i1 = uniqueSecond(root, visitsBefore, all, i0);
-    if (i1 < 0) return false;
-    const PuctNode* n0 = root->getNodeChild(0, i0)->to_node;
-    const PuctNode* n1 = root->getNodeChild(0, i1)->to_node;
+    // one pass: the first two places under visitsBefore with their multiplicities; both must be
+    // unique for the sorted order's first two elements to be order-independent
+    const PuctNodeChild* cs = root->children();
+    const PuctNodeChild *a = nullptr, *b = nullptr;
+    int a_n = 0, b_n = 0;
+    for (int i = 0; i < n; ++i) {
+        const PuctNodeChild* c = cs + i;
+        if (a == nullptr) {
+            a = c;
+            a_n = 1;
+        } else if (visitsBefore(c, a)) {
+            b = a;
+            b_n = a_n;
+            a = c;
+            a_n = 1;
+        } else if (!visitsBefore(a, c)) {
+            a_n++;
+        } else if (b == nullptr || visitsBefore(c, b)) {
+            b = c;
+            b_n = 1;
+        } else if (!visitsBefore(b, c)) {
+            b_n++;
+        }
+    }
+    if (a_n != 1 || b == nullptr || b_n != 1) return false;
+    const PuctNode* n0 = a->to_node;
+    const PuctNode* n1 = b->to_node;
     bool r = false;
     if (n0 != nullptr && n1 != nullptr) {
         const int role_index = root->lead_role_index;
@@ -374,162 +389,60 @@ static inline bool selectBefore(const PuctNodeChild* a, const PuctNodeChild* b, 
 // its position in the sorted order is the number of reaching children that sort strictly before it,
 // which is order-independent unless another reaching child ties with d under the comparator (then
 // the literal path runs).  The draws are made in the same number, d's is the one at that position.
-bool PuctEvaluator::selectChildFast(PuctNode* node, int depth, float prior_score, double sqrt_node_visits,
-                                    PuctNodeChild** out) {
-    const bool latch = node->visits > 1000 && node->visits < 40000000 && depth == 0;
-    const float limit_latch_root = 0.66;
-    const int n = node->num_children;
-    if (n > 512) return false;
-    double scores[512];
-    const int lead = node->lead_role_index;
-    int win = -1;
-    bool win_tied = false;
-    float win_key = 0.f;
-    int best = -1;
-    double best_score = 0.0;
-    int latch_d = -1, reach = 0;
-    PuctNodeChild* cs = node->children();
-    for (int i = 0; i < n; ++i) {
-        PuctNodeChild* c = cs + i;
-        scores[i] = -1e300;    // not a candidate
-        if (c->unselectable) continue;
-        const PuctNode* cn = c->to_node;
-        if (cn != nullptr && cn->num_children > 0 && cn->unselectable_count == cn->num_children) continue;
-        double child_score = prior_score;
-        const int traversals = c->traversals + 1;
-        const double inflight_visits = cn != nullptr ? cn->inflight_visits : 0;
-        if (c->traversals > 0 && inflight_visits > 0) return false;                  // discount draws RNG
-        double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
-                                   (traversals + inflight_visits);
-        if (cn != nullptr) {
-            child_score = cn->getCurrentScore(lead);
-            if (cn->is_finalised) {
-                if (child_score > 0.99) {
-                    if (depth > 0) {
-                        // the first win in sortedChildrenSelect order has the highest current score
-                        const float k = cn->getCurrentScore(lead);
-                        if (win < 0 || k > win_key) {
-                            win = i;
-                            win_key = k;
-                            win_tied = false;
-                        } else if (k == win_key) {
-                            win_tied = true;
-                        }
-                        continue;
-                    }
-                    child_score *= 1.0f + node->puct_constant;
-                } else if (child_score < 0.01) {
-                    continue;   // bad_fallback candidate
-                } else {
-                    exploration_score = 0.0;
-                }
-            }
-        }
-        const double score = child_score + exploration_score;
-        scores[i] = score;
-        ++reach;
-        if (latch && c->traversals > 16 && c->traversals > node->visits * limit_latch_root) {
-            if (latch_d >= 0) return false;
-            latch_d = i;
-        }
-        if (best < 0 || score > best_score) {
-            best = i;
-            best_score = score;
-        }
-    }
-    if (win >= 0) {
-        if (win_tied) return false;
-        *out = cs + win;
-        return true;
-    }
-    if (best < 0 || !(best_score > -1.0)) return false;
-    Rng saved_rng = rng;
-    if (latch) {
-        int rank = 0;
-        if (latch_d >= 0) {
-            if (reach < 2) return false;   // d alone: the fallback rules decide
-            const PuctNodeChild* d = cs + latch_d;
-            for (int i = 0; i < n; ++i) {
-                if (i == latch_d || scores[i] == -1e300) continue;
-                if (selectBefore(cs + i, d, lead)) ++rank;
-                else if (!selectBefore(d, cs + i, lead)) return false;   // tie: position undetermined
-            }
-        }
-        bool latched = false;
-        for (int j = 0; j < reach; ++j) {
-            const double v = rng.get();
-            if (j == rank && latch_d >= 0 && v > 0.1) latched = true;
-        }
-        if (latched) {
-            scores[latch_d] = -1e300;
-            best = -1;
-            for (int i = 0; i < n; ++i) {
-                if (scores[i] == -1e300) continue;
-                if (best < 0 || scores[i] > best_score) {
-                    best = i;
-                    best_score = scores[i];
-                }
-            }
-            if (best < 0 || !(best_score > -1.0)) {
-                rng = saved_rng;
-                return false;
-            }
-        }
-    }
-    // order independence of `if (score > best_score_float)`: the max m must replace any incumbent
-    // (m > float(c)) and never be replaced (c <= float(m)).
-    const double fm = (float)best_score;
-    for (int i = 0; i < n; ++i) {
-        if (i == best || scores[i] == -1e300) continue;
-        const double sc = scores[i];
-        if (sc > fm || !(best_score > (double)(float)sc)) {
-            rng = saved_rng;
-            return false;
-        }
-    }
-    *out = cs + best;
-    return true;
-}
+// ---- child selection --------------------------------------------------------------------------
+// Per-thread scratch of the selection pass (every evaluator of a thread runs on that thread; nothing
+// here is live across a coroutine switch).
+namespace {
+struct SelectScratch {
+    std::vector<double> base, expl, inflight, scores;
+    std::vector<uint32_t> trav;
+    std::vector<uint8_t> kind, bcs;
+    std::vector<float> key_s, key_p;
+    // sortedChildrenSelect permutation cache, keyed by the sort's input keys only: std::sort's
+    // permutation is a function of the sequence of comparison outcomes, hence of the keys
+    std::vector<float> cached_s, cached_p;
+    std::vector<uint16_t> perm;
+    int cached_n = -1;
+    struct Key {
+        float s, p;
+        uint16_t i;
+    };
+    std::vector<Key> tmp;
 
-// evaluator.cpp:341-517
-PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
-    GZ_ASSERT(!node->isTerminal());
-    const int depth = (int)path.size();
-    setPuctConstant(node, depth);
-
-    if (node->num_children == 1) {
-        PuctNodeChild* child = node->getNodeChild(0, 0);
-        path.emplace_back(node, child, child);
-        return child;
+    void reserve(int n) {
+        if ((int)base.size() >= n) return;
+        base.resize(n); expl.resize(n); inflight.resize(n); scores.resize(n); trav.resize(n);
+        kind.resize(n); bcs.resize(n); key_s.resize(n); key_p.resize(n); perm.resize(n); tmp.resize(n);
+        cached_s.resize(n); cached_p.resize(n);
     }
 
-    if (depth == 0) setDirichletNoise(node);
-
-    const float prior_score = priorScore(node, depth);
-    const double sqrt_node_visits = std::sqrt(node->visits + 1);
-
-    PuctNodeChild* fast_choice = nullptr;
-    const Rng rng_before = rng;
-    const bool fast_ok = selectChildFast(node, depth, prior_score, sqrt_node_visits, &fast_choice);
-    if (fast_ok && !verify_fastpath()) {
-        path.emplace_back(node, fast_choice, fast_choice);
-        return fast_choice;
+    const uint16_t* sortedOrder(int n) {
+        if (n == cached_n && std::memcmp(key_s.data(), cached_s.data(), n * sizeof(float)) == 0 &&
+            std::memcmp(key_p.data(), cached_p.data(), n * sizeof(float)) == 0)
+            return perm.data();
+        for (int i = 0; i < n; ++i) tmp[i] = Key{key_s[i], key_p[i], (uint16_t)i};
+        std::sort(tmp.begin(), tmp.begin() + n, [](const Key& a, const Key& b) {
+            if (a.s < 0 && b.s < 0) return a.p > b.p;
+            return a.s > b.s;
+        });
+        for (int i = 0; i < n; ++i) perm[i] = tmp[i].i;
+        std::memcpy(cached_s.data(), key_s.data(), n * sizeof(float));
+        std::memcpy(cached_p.data(), key_p.data(), n * sizeof(float));
+        cached_n = n;
+        return perm.data();
     }
-    // verification: replay the literal loop from the same RNG state; it must end in the same state
-    const Rng rng_after_fast = rng;
-    rng = rng_before;
-    struct RngCheck {
-        const Rng& fast_state;
-        const Rng& live;
-        bool active;
-        ~RngCheck() {
-            if (active && !(fast_state == live)) {
-                std::fprintf(stderr, "gz fast-path selectChild RNG mismatch\n");
-                std::abort();
-            }
-        }
-    } rng_check{rng_after_fast, rng, fast_ok};
+};
+thread_local SelectScratch t_sel;
 
+// child kinds of the selection pass
+enum : uint8_t { kSkip = 0, kPrior = 1, kScored = 2, kWinReturn = 3, kBad = 4 };
+}  // namespace
+
+// The literal selection loop of the reference over sortedChildrenSelect (evaluator.cpp:341-517),
+// kept verbatim for the verification mode (GZ_VERIFY_FASTPATH=1) and for nodes with > 65535
+// children.  Returns the chosen child (or null) and its best-score companion in *best_out.
+PuctNodeChild* PuctEvaluator::selectChildLiteral(PuctNode* node, int depth, float prior_score,
+                                                 double sqrt_node_visits, PuctNodeChild** best_out) {
     float best_score = -1;
     PuctNodeChild* best_child = nullptr;
     float best_child_score_actual_score = -1;
@@ -562,11 +475,7 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
             if (cn->is_finalised) {
                 if (child_score > 0.99) {
                     if (depth > 0) {
-                        if (fast_ok && c != fast_choice) {
-                            std::fprintf(stderr, "gz fast-path selectChild (win) mismatch\n");
-                            std::abort();
-                        }
-                        path.emplace_back(node, c, c);
+                        *best_out = c;
                         return c;
                     }
                     child_score *= 1.0f + node->puct_constant;
@@ -620,12 +529,299 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
         }
     }
     if (best_child_score == nullptr) best_child_score = best_child;
-    if (fast_ok && best_child != fast_choice) {
-        std::fprintf(stderr, "gz fast-path selectChild mismatch\n");
-        std::abort();
-    }
-    if (best_child != nullptr) path.emplace_back(node, best_child, best_child_score);
+    *best_out = best_child_score;
     return best_child;
+}
+
+// selectChild (evaluator.cpp:341-517).  One pass over the children gathers everything the
+// reference computes from them: priorScore's chooseTopVisits scan and FPU policy sum
+// (evaluator.cpp:1195-1224), each child's selection terms and its sort key.  Then:
+//   1. when the winner provably does not depend on the order the reference's std::sort produces
+//      (no RNG-dependent step, strictly separated maximum), it is returned directly;
+//   2. otherwise the reference's loop runs over the gathered arrays in sortedChildrenSelect order,
+//      with the permutation recomputed only when a sort key changed (in the spinning phases of
+//      self-play -- the root re-selecting finalised children -- the keys repeat for thousands of
+//      playouts); RNG draws (inflight discount, root latch) happen exactly as in the reference.
+PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
+    GZ_ASSERT(!node->isTerminal());
+    const int depth = (int)path.size();
+    setPuctConstant(node, depth);
+
+    if (node->num_children == 1) {
+        PuctNodeChild* child = node->getNodeChild(0, 0);
+        path.emplace_back(node, child, child);
+        return child;
+    }
+
+    if (depth == 0) setDirichletNoise(node);
+
+    const double sqrt_node_visits = std::sqrt(node->visits + 1);
+    const int n = node->num_children;
+    if (n > 65535) {
+        PuctNodeChild* best = nullptr;
+        PuctNodeChild* chosen = selectChildLiteral(node, depth, priorScore(node, depth), sqrt_node_visits, &best);
+        if (chosen != nullptr) path.emplace_back(node, chosen, best);
+        return chosen;
+    }
+
+    SelectScratch& S = t_sel;
+    S.reserve(n);
+    const int lead = node->lead_role_index;
+    PuctNodeChild* cs = node->children();
+    const bool latch = node->visits > 1000 && node->visits < 40000000 && depth == 0;
+    const float limit_latch_root = 0.66;
+
+    const bool want_top = node->visits > 8;
+    TopVisitsScan top;
+    float total_policy_visited = 0.0;
+    int win = -1;
+    bool win_tied = false, rng_steps = false;
+    float win_key = 0.f;
+    int latch_d = -1, latch_count = 0, reach = 0;
+    for (int i = 0; i < n; ++i) {
+        PuctNodeChild* c = cs + i;
+        const PuctNode* cn = c->to_node;
+        if (want_top) top.add(c, lead);
+        if (cn != nullptr && cn->visits > 0) total_policy_visited += c->policy_prob;
+        S.key_s[i] = cn == nullptr ? -1 : cn->getCurrentScore(lead);
+        S.key_p[i] = c->policy_prob_orig;
+
+        S.kind[i] = kSkip;
+        if (c->unselectable) continue;
+        if (cn != nullptr && cn->num_children > 0 && cn->unselectable_count == cn->num_children) continue;
+        const int traversals = c->traversals + 1;
+        const double inflight_visits = cn != nullptr ? cn->inflight_visits : 0;
+        double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
+                                   (traversals + inflight_visits);
+        S.trav[i] = c->traversals;
+        S.inflight[i] = inflight_visits;
+        if (c->traversals > 0 && inflight_visits > 0) rng_steps = true;   // discount draws RNG
+        if (cn != nullptr) {
+            double child_score = cn->getCurrentScore(lead);
+            if (cn->is_finalised) {
+                if (child_score > 0.99) {
+                    if (depth > 0) {
+                        // the first win in sortedChildrenSelect order has the highest current score
+                        S.kind[i] = kWinReturn;
+                        const float k = cn->getCurrentScore(lead);
+                        if (win < 0 || k > win_key) {
+                            win = i;
+                            win_key = k;
+                            win_tied = false;
+                        } else if (k == win_key) {
+                            win_tied = true;
+                        }
+                        continue;
+                    }
+                    child_score *= 1.0f + node->puct_constant;
+                } else if (child_score < 0.01) {
+                    S.kind[i] = kBad;   // bad_fallback candidate
+                    continue;
+                } else {
+                    exploration_score = 0.0;
+                }
+            }
+            S.kind[i] = kScored;
+            S.base[i] = child_score;
+            S.bcs[i] = cn->is_finalised || cn->visits > 42;
+        } else {
+            S.kind[i] = kPrior;
+        }
+        S.expl[i] = exploration_score;
+        ++reach;
+        if (latch && c->traversals > 16 && c->traversals > node->visits * limit_latch_root) {
+            ++latch_count;
+            latch_d = i;
+        }
+    }
+
+    // priorScore (evaluator.cpp:1195-1224)
+    float prior_score = node->getFinalScore(lead);
+    if (want_top) {
+        const PuctNodeChild* best_top = nullptr;
+        if (!top.finish(lead, conf->top_visits_best_guess_converge_ratio, &best_top)) best_top = chooseTopVisitsExact(node);
+        if (best_top->to_node != nullptr) prior_score = best_top->to_node->getCurrentScore(lead);
+    }
+    {
+        float fpu_reduction = depth == 0 ? conf->fpu_prior_discount_root : conf->fpu_prior_discount;
+        if (fpu_reduction > 0) {
+            fpu_reduction *= std::sqrt(total_policy_visited);
+            prior_score -= fpu_reduction;
+        }
+    }
+
+    const bool verify = verify_fastpath();
+    const Rng rng_before = rng;
+    PuctNodeChild* chosen = nullptr;
+    PuctNodeChild* chosen_best = nullptr;
+    bool done = false;
+
+    // 1. order-independent outcome
+    if (win >= 0) {
+        if (!win_tied && !rng_steps) {
+            chosen = chosen_best = cs + win;
+            done = true;
+        }
+    } else if (!rng_steps && latch_count <= 1) {
+        int best = -1;
+        double best_score = 0.0;
+        for (int i = 0; i < n; ++i) {
+            if (S.kind[i] != kPrior && S.kind[i] != kScored) {
+                S.scores[i] = -1e300;   // not a candidate
+                continue;
+            }
+            const double child_score = S.kind[i] == kPrior ? (double)prior_score : S.base[i];
+            const double score = child_score + S.expl[i];
+            S.scores[i] = score;
+            if (best < 0 || score > best_score) {
+                best = i;
+                best_score = score;
+            }
+        }
+        bool ok = best >= 0 && best_score > -1.0;
+        if (ok && latch) {
+            // root latch: only d's draw matters; its rank among the reaching children in sorted
+            // order must be determined without the sort (no reaching child ties with d)
+            int rank = 0;
+            if (latch_d >= 0) {
+                if (reach < 2) ok = false;   // d alone: the fallback rules decide
+                const PuctNodeChild* d = cs + latch_d;
+                for (int i = 0; ok && i < n; ++i) {
+                    if (i == latch_d || S.scores[i] == -1e300) continue;
+                    if (selectBefore(cs + i, d, lead)) ++rank;
+                    else if (!selectBefore(d, cs + i, lead)) ok = false;   // tie: position undetermined
+                }
+            }
+            if (ok) {
+                bool latched = false;
+                for (int j = 0; j < reach; ++j) {
+                    const double v = rng.get();
+                    if (j == rank && latch_d >= 0 && v > 0.1) latched = true;
+                }
+                if (latched) {
+                    S.scores[latch_d] = -1e300;
+                    best = -1;
+                    for (int i = 0; i < n; ++i) {
+                        if (S.scores[i] == -1e300) continue;
+                        if (best < 0 || S.scores[i] > best_score) {
+                            best = i;
+                            best_score = S.scores[i];
+                        }
+                    }
+                    ok = best >= 0 && best_score > -1.0;
+                }
+            }
+        }
+        if (ok) {
+            // order independence of `if (score > best_score_float)`: the max m must replace any
+            // incumbent (m > float(c)) and never be replaced (c <= float(m)).
+            const double fm = (float)best_score;
+            for (int i = 0; i < n; ++i) {
+                if (i == best || S.scores[i] == -1e300) continue;
+                const double sc = S.scores[i];
+                if (sc > fm || !(best_score > (double)(float)sc)) {
+                    ok = false;
+                    break;
+                }
+            }
+        }
+        if (ok) {
+            chosen = chosen_best = cs + best;
+            done = true;
+        } else {
+            rng = rng_before;
+        }
+    }
+
+    // 2. the reference's loop in sorted order over the gathered terms
+    if (!done) {
+        const uint16_t* order = S.sortedOrder(n);
+        float best_score = -1;
+        PuctNodeChild* best_child = nullptr;
+        float best_child_score_actual_score = -1;
+        PuctNodeChild* best_child_score = nullptr;
+        PuctNodeChild* bad_fallback = nullptr;
+        float best_fallback_score = -1;
+        PuctNodeChild* best_fallback = nullptr;
+        int unselectables = 0;
+        bool returned = false;
+        for (int k = 0; k < n; ++k) {
+            const int i = order[k];
+            PuctNodeChild* c = cs + i;
+            const uint8_t kd = S.kind[i];
+            if (kd == kSkip) {
+                unselectables++;
+                continue;
+            }
+            if (kd == kWinReturn) {
+                chosen = chosen_best = c;
+                returned = true;
+                break;
+            }
+            if (kd == kBad) {
+                bad_fallback = c;
+                continue;
+            }
+            double child_score = kd == kPrior ? (double)prior_score : S.base[i];
+            const double exploration_score = S.expl[i];
+            if (kd == kScored && S.bcs[i] && child_score > best_child_score_actual_score) {
+                best_child_score_actual_score = child_score;
+                best_child_score = c;
+            }
+            const double inflight_visits = S.inflight[i];
+            const uint32_t trav = S.trav[i];
+            if (trav > 0 && inflight_visits > 0) {
+                const double discounted_visits = inflight_visits * (rng.get() + 0.5);
+                child_score = (child_score * trav) / (trav + discounted_visits);
+            }
+            c->debug_node_score = child_score;
+            c->debug_puct_score = exploration_score;
+            const double score = child_score + exploration_score;
+            if (latch && rng.get() > 0.1) {
+                if (trav > 16 && trav > node->visits * limit_latch_root) {
+                    if (best_fallback == nullptr || score > best_fallback_score) {
+                        best_fallback = c;
+                        best_fallback_score = score;
+                    }
+                    continue;
+                }
+            }
+            if (score > best_score) {
+                best_child = c;
+                best_score = score;
+            }
+        }
+        if (!returned) {
+            if (best_child == nullptr) {
+                if (best_fallback != nullptr) {
+                    best_child = best_child_score != nullptr ? best_child_score : best_fallback;
+                } else if (bad_fallback != nullptr) {
+                    if (unselectables > 0) scheduler->yield();
+                    best_child = bad_fallback;
+                } else {
+                    stats.num_blocked++;
+                }
+            }
+            if (best_child_score == nullptr) best_child_score = best_child;
+            chosen = best_child;
+            chosen_best = best_child_score;
+        }
+    }
+
+    if (verify) {
+        // replay the literal reference loop from the same RNG state: same child, same RNG state
+        const Rng rng_after = rng;
+        rng = rng_before;
+        const float exact_prior = priorScore(node, depth);
+        PuctNodeChild* lit_best = nullptr;
+        PuctNodeChild* lit = selectChildLiteral(node, depth, exact_prior, sqrt_node_visits, &lit_best);
+        if (!(exact_prior == prior_score) || lit != chosen || !(rng == rng_after)) {
+            std::fprintf(stderr, "gz selectChild verification mismatch (depth %d, n %d)\n", depth, n);
+            std::abort();
+        }
+    }
+    if (chosen != nullptr) path.emplace_back(node, chosen, chosen_best);
+    return chosen;
 }
 
 // evaluator.cpp:519-656
@@ -767,7 +963,13 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
     int evals_seen = stats.num_evaluations, quiet_playouts = 0;   // spin_yield_playouts (config.h)
     while (true) {
         const int our_role_index = root->lead_role_index;
-        const bool is_converged = converged(conf->converged_visits);
+        // converged() is pure (no RNG, no writes); the reference evaluates it every iteration, but
+        // without think time its value can only matter once tree playouts exceed max_tree_playouts
+        // or evaluations exceed either evaluation limit, so it is evaluated lazily (same decisions).
+        const bool need_converged = use_think_time || stats.num_tree_playouts > max_tree_playouts ||
+                                    stats.num_evaluations > max_evaluations ||
+                                    stats.num_evaluations > max_non_converged_evaluations;
+        const bool is_converged = need_converged ? converged(conf->converged_visits) : false;
 
         if (end_time > 0 && get_time() > end_time) break;
         if (root->is_finalised && stats.num_tree_playouts > 100) break;

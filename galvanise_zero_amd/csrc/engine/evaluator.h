@@ -86,7 +86,8 @@ private:
     PuctNode* lookupNode(const uint64_t* bs, int depth);
     PuctNode* createNode(PuctNode* parent, const uint64_t* state);
     PuctNodeChild* selectChild(PuctNode* node, Path& path);
-    bool selectChildFast(PuctNode* node, int depth, float prior_score, double sqrt_node_visits, PuctNodeChild** out);
+    PuctNodeChild* selectChildLiteral(PuctNode* node, int depth, float prior_score, double sqrt_node_visits,
+                                      PuctNodeChild** best_out);
     bool chooseTopVisitsFast(const PuctNode* node, const PuctNodeChild** out) const;
     const PuctNodeChild* chooseTopVisitsExact(const PuctNode* node) const;
     bool convergedFast(int count, bool* out) const;
