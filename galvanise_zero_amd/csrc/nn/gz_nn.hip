@@ -516,3 +516,5 @@ extern "C" int gz_net_stamp_avg(const gz_net* net, double* out8) {
 }
 
 extern "C" float gz_net_last_kernel_ms(const gz_net* net) { return net ? net->last_ms : 0.f; }
+
+extern "C" int gz_net_large_min_rows(const gz_net* net) { return net ? net->large_min_rows : 0; }

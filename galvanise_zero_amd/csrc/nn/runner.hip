@@ -75,6 +75,9 @@ struct gz_runner {
     std::atomic<bool> stop{false};
     std::atomic<long> batches{0}, rows{0}, launches{0}, samples_taken{0}, segments{0};
     std::atomic<long> kernel_us{0}, trunk_us{0};
+    // launches that ran the multi-board trunk variant (rows >= gz_net_large_min_rows)
+    std::atomic<long> large_launches{0}, large_rows{0}, large_trunk_us{0};
+    int large_min_rows = 1 << 30;
     std::mutex m;
     std::condition_variable cv;
     std::atomic<int> failed{0};
@@ -170,8 +173,14 @@ static void launcher_main(gz_runner* r) {
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, b.ev0, b.ev1) == hipSuccess)
                 r->kernel_us.fetch_add((long)(ms * 1000.0f), std::memory_order_relaxed);
-            if (hipEventElapsedTime(&ms, b.ev0, b.evm) == hipSuccess)
+            if (hipEventElapsedTime(&ms, b.ev0, b.evm) == hipSuccess) {
                 r->trunk_us.fetch_add((long)(ms * 1000.0f), std::memory_order_relaxed);
+                if (b.rows >= r->large_min_rows) {
+                    r->large_launches.fetch_add(1, std::memory_order_relaxed);
+                    r->large_rows.fetch_add(b.rows, std::memory_order_relaxed);
+                    r->large_trunk_us.fetch_add((long)(ms * 1000.0f), std::memory_order_relaxed);
+                }
+            }
             for (int i : b.pools) {
                 Pool& p = r->pools[i];
                 p.rows_done = p.rows;
@@ -274,6 +283,7 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
     r->num_policies = num_policies;
     r->num_values = num_values;
     r->policy_sizes.assign(policy_sizes, policy_sizes + num_policies);
+    r->large_min_rows = gz_net_large_min_rows(net);
     bool ok = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess;
     for (Batch& b : r->batches_ring)
         ok = ok && hipEventCreate(&b.ev0) == hipSuccess && hipEventCreate(&b.evm) == hipSuccess &&
@@ -365,6 +375,9 @@ extern "C" int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out) {
     out->rows = r->rows.load();
     out->kernel_ms = r->kernel_us.load() / 1000.0;
     out->trunk_ms = r->trunk_us.load() / 1000.0;
+    out->large_launches = r->large_launches.load();
+    out->large_rows = r->large_rows.load();
+    out->large_trunk_ms = r->large_trunk_us.load() / 1000.0;
     out->kernel_launches = r->launches.load();
     out->samples = r->samples_taken.load();
     out->segments = r->segments.load();

@@ -85,6 +85,10 @@ int gz_net_forward_device(gz_net* net, void* stream, const float* d_planes, int 
 /* Device time (ms) of the last gz_net_forward (both launches), measured with HIP events on its stream. */
 float gz_net_last_kernel_ms(const gz_net* net);
 
+/* Launches of at least this many rows run the two-boards-per-workgroup trunk variant, smaller ones
+ * the one-board variant (both compute every row identically). */
+int gz_net_large_min_rows(const gz_net* net);
+
 /* Algorithmic FLOPs of one leaf evaluation (2 FLOP/MAC). */
 double gz_net_flops_per_eval(const gz_net* net);
 
@@ -135,6 +139,9 @@ typedef struct gz_runner_stats {
     long dupes;
     long segments;               /* pools merged into launches, summed over launches */
     long completed_game_evals;   /* NN evaluations consumed by the completed games */
+    long large_launches;         /* launches that ran the two-boards-per-workgroup trunk variant */
+    long large_rows;
+    double large_trunk_ms;
 } gz_runner_stats;
 
 gz_runner* gz_runner_create(gz_net* net, const struct gz_sm* sm, const struct gz_transformer* t,

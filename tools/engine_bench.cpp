@@ -1,9 +1,12 @@
-// Host-only engine throughput probe: one pool of breakthrough self-play driven by a synthetic
-// network (random policy / value), no GPU.  Reports microseconds of tree work per leaf.
+// Host-only engine throughput probe: T threads x one pool of breakthrough self-play each, driven by a
+// synthetic network (random policy / value), no GPU.  Reports microseconds of tree work per leaf.
+// Usage: engine_bench [batch] [polls] [evals] [threads] [spin_yield]
 //   g++ -O2 -std=c++17 -ffp-contract=off -march=x86-64-v3 tools/engine_bench.cpp galvanise_zero_amd/csrc/engine/*.cpp -o /tmp/engine_bench -pthread
 #include "../include/gzero_engine.h"
 
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -21,10 +24,7 @@ static gz_puct_config base_puct(float noise) {
     return c;
 }
 
-int main(int argc, char** argv) {
-    const int B = argc > 1 ? atoi(argv[1]) : 256;
-    const int polls = argc > 2 ? atoi(argv[2]) : 2000;
-    const int evals = argc > 3 ? atoi(argv[3]) : 800;
+static void run(int tid, int B, int polls, int evals, int spin) {
     gz_sm* sm = gz_sm_create("breakthrough");
     int ps[2] = {155, 155};
     gz_transformer* t = gz_transformer_create(64, 2, 1, 1, 2, ps, 2);
@@ -36,7 +36,7 @@ int main(int argc, char** argv) {
     gz_transformer_add_control_base(t, 129, 0, 0.0f);
     std::vector<float> planes((size_t)B * 320), pol0((size_t)B * 155), pol1((size_t)B * 155), val((size_t)B * 2);
     float* pols[2] = {pol0.data(), pol1.data()};
-    gz_pool* pool = gz_pool_create(sm, t, B, "bench", 1, 0, nullptr, planes.data(), pols, val.data());
+    gz_pool* pool = gz_pool_create(sm, t, B, "bench", 1, (long)tid * B, nullptr, planes.data(), pols, val.data());
     gz_selfplay_config conf{};
     conf.oscillate_sampling_pct = 0.25f; conf.temperature_for_policy = 1.0f; conf.puct_config = base_puct(0.25f);
     conf.evals_per_move = evals; conf.resign0_score_probability = 0.1f; conf.resign0_pct = 0.99f;
@@ -45,12 +45,15 @@ int main(int argc, char** argv) {
     conf.run_to_end_evals = 32; conf.run_to_end_puct_config = base_puct(0.15f);
     conf.run_to_end_puct_config.random_scale = 0.75f; conf.run_to_end_early_score = 0.01f;
     conf.run_to_end_minimum_game_depth = 30;
+    conf.puct_config.spin_yield_playouts = spin;
+    conf.run_to_end_puct_config.spin_yield_playouts = spin;
     gz_pool_start(pool, &conf);
-    std::mt19937 rng(1);
+    std::mt19937 rng(1 + tid);
     std::uniform_real_distribution<float> U(0.f, 1.f);
     int rows = gz_pool_poll(pool, 0);
     long leaves = 0;
-    double tt = 0, worst = 0;
+    double tt = 0, worst = 0, win_t = 0;
+    long win_l = 0;
     for (int i = 0; i < polls; ++i) {
         for (int r = 0; r < rows; ++r) {
             float s0 = 0, s1 = 0;
@@ -63,11 +66,33 @@ int main(int argc, char** argv) {
         rows = gz_pool_poll(pool, done);
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
         if (i >= 50) { tt += dt; leaves += done; if (dt > worst) worst = dt; }
+        win_t += dt;
+        win_l += done;
+        if (tid == 0 && (i + 1) % 2000 == 0) {
+            std::printf("thread 0 polls %6d: window %.2f us/leaf\n", i + 1, win_t / win_l * 1e6);
+            std::fflush(stdout);
+            win_t = 0;
+            win_l = 0;
+        }
     }
     gz_pool_stats st;
     gz_pool_get_stats(pool, &st);
-    std::printf("B=%d polls=%d: %.3f us/leaf, worst poll %.1f ms, games completed %ld, samples %ld\n", B, polls,
+    std::printf("thread %d B=%d polls=%d: %.3f us/leaf, worst poll %.1f ms, games completed %ld, samples %ld\n", tid, B, polls,
                 tt / leaves * 1e6, worst * 1e3, st.games_completed, st.samples);
     gz_pool_destroy(pool);
+}
+
+int main(int argc, char** argv) {
+    const int B = argc > 1 ? atoi(argv[1]) : 256;
+    const int polls = argc > 2 ? atoi(argv[2]) : 2000;
+    const int evals = argc > 3 ? atoi(argv[3]) : 800;
+    const int threads = argc > 4 ? atoi(argv[4]) : 1;
+    const int spin = argc > 5 ? atoi(argv[5]) : 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> ts;
+    for (int i = 0; i < threads; ++i) ts.emplace_back(run, i, B, polls, evals, spin);
+    for (auto& t : ts) t.join();
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("%d threads: %.1f s wall, %.0f leaves/s total\n", threads, el, (double)threads * B * polls / el);
     return 0;
 }
