@@ -30,10 +30,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0      # gfx950 dense bf16 MFMA (MI355X_MICROARCH.md)
-# PMC-measured fabric bytes per trunk launch (FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc
-# passes, tools/profile_bench.sh); None until measured for the current kernel.
-TRAFFIC_PER_LAUNCH = None
-TRAFFIC_SOURCE = None
+# PMC-measured fabric bytes per trunk launch (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE,
+# separate rocprofv3 --pmc passes of tools/profile_bench.sh at 256 / 512 rows, profiles/r01d_pmc.txt).
+# PMC counters cannot be read inside the timed run, so the measured per-launch figure of the same
+# kernel at the bench's launch size is reported.
+TRAFFIC_PER_LAUNCH = {"gznn::trunk_kernel<128, 8, 8, 1, 1>": (14290.1 * 2 + 320.0) * 1024,
+                      "gznn::trunk_kernel<128, 8, 8, 2, 1>": (14581.6 * 2 + 640.0) * 1024}
+TRAFFIC_SOURCE = "profiles/r01d_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 256- and 512-row launches)"
 
 
 def parse():
@@ -215,9 +218,8 @@ def main():
             "value": rows / T,
             "unit": "leaf-evals/s",
             "games_per_sec": games / T,
-            # steady state: leaf-evals/s / mean NN evaluations per completed game (all games since start)
-            "games_per_sec_steady": (rows / T) / (game_evals_all / games_all) if games_all else None,
-            "evals_per_game": game_evals_all / games_all if games_all else None,
+            # mean NN evaluations of the games completed since start (biased to short games early on)
+            "evals_per_completed_game": game_evals_all / games_all if games_all else None,
             "games_completed_total": games_all,
             "sample_games_per_sec": games_s / T,
             "samples_per_sec": samples / T,
@@ -235,7 +237,8 @@ def main():
                        "games_per_gpu": npools * args.batch, "threads_per_gpu": threads,
                        "pools_per_thread": args.pools, "eval_batch": args.batch, "parallelism": "games sharded dp%d" % world},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": TRAFFIC_PER_LAUNCH,
+                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": TRAFFIC_PER_LAUNCH.get(dom),
+                         "traffic_unit": "bytes/launch",
                          "traffic_source": TRAFFIC_SOURCE,
                          "kernel": dom, "avg_kernel_ms": per_variant[dom]["avg_kernel_ms"] if dom else None,
                          "rows_per_launch": per_variant[dom]["rows_per_launch"] if dom else None,
