@@ -191,10 +191,10 @@ def main():
     totals, T = shard.reduce_counters(
         [d["rows"], d["batches"], d["games_completed"], d["games_with_samples"], d["samples"], d["kernel_ms"],
          d["kernel_launches"], d["segments"], s1["games_completed"], s1["completed_game_evals"], d["trunk_ms"],
-         d["large_launches"], d["large_rows"], d["large_trunk_ms"]],
+         d["large_launches"], d["large_rows"], d["large_trunk_ms"], d["engine_idle_ms"]],
         elapsed, device="cuda")
     (rows, batches, games, games_s, samples, kms, launches, segments, games_all, game_evals_all, tms,
-     l_launches, l_rows, l_tms) = totals
+     l_launches, l_rows, l_tms, idle_ms) = totals
 
     if rank == 0:
         flops = desc.flops_per_eval()
@@ -249,6 +249,7 @@ def main():
                          "forward_tflops": flops * rows_per_launch / avg_fwd_s / 1e12,
                          "flop_per_leaf": flops, "aggregate_tflops": flops * rows / T / 1e12},
             "gpu_busy_frac": (kms / 1e3) / (T * world) if T > 0 else None,
+            "engine_idle_frac": (idle_ms / 1e3) / (T * world * threads) if T > 0 else None,
             "host_peak_rss_gb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6,
         }
         if world == 1 and not args.no_cpu_baseline:

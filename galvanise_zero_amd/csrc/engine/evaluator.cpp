@@ -663,8 +663,10 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
             done = true;
         }
     } else if (!rng_steps && latch_count <= 1) {
-        int best = -1;
-        double best_score = 0.0;
+        // scores and the three best candidates (enough to decide strict separation both for the
+        // full candidate set and for the set without the latch candidate d)
+        int i1 = -1, i2 = -1, i3 = -1;
+        double v1 = 0.0, v2 = 0.0, v3 = 0.0;
         for (int i = 0; i < n; ++i) {
             if (S.kind[i] != kPrior && S.kind[i] != kScored) {
                 S.scores[i] = -1e300;   // not a candidate
@@ -673,24 +675,55 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
             const double child_score = S.kind[i] == kPrior ? (double)prior_score : S.base[i];
             const double score = child_score + S.expl[i];
             S.scores[i] = score;
-            if (best < 0 || score > best_score) {
-                best = i;
-                best_score = score;
+            // ties keep the earlier index first; separation below rejects near-ties anyway
+            if (i1 < 0 || score > v1) {
+                i3 = i2; v3 = v2;
+                i2 = i1; v2 = v1;
+                i1 = i; v1 = score;
+            } else if (i2 < 0 || score > v2) {
+                i3 = i2; v3 = v2;
+                i2 = i; v2 = score;
+            } else if (i3 < 0 || score > v3) {
+                i3 = i; v3 = score;
             }
         }
-        bool ok = best >= 0 && best_score > -1.0;
+        // order independence of `if (score > best_score_float)`: the max m must replace any
+        // incumbent (m > float(c)) and never be replaced (c <= float(m)); float rounding is
+        // monotone, so checking the runner-up suffices
+        auto separated = [](int ib, double vb, int ir, double vr) {
+            if (ib < 0 || !(vb > -1.0)) return false;
+            if (ir < 0) return true;
+            const double fm = (float)vb;
+            return !(vr > fm) && vb > (double)(float)vr;
+        };
+        const bool sep_all = separated(i1, v1, i2, v2);
+        int j1 = i1, j2 = i2;
+        double w1 = v1, w2 = v2;
+        if (latch_d >= 0) {   // the set without d
+            if (i1 == latch_d) { j1 = i2; w1 = v2; j2 = i3; w2 = v3; }
+            else if (i2 == latch_d) { j2 = i3; w2 = v3; }
+        }
+        const bool sep_no_d = latch_d >= 0 && separated(j1, w1, j2, w2);
+
+        bool ok = sep_all || sep_no_d;
+        int best = i1;
         if (ok && latch) {
             // root latch: only d's draw matters; its rank among the reaching children in sorted
             // order must be determined without the sort (no reaching child ties with d)
             int rank = 0;
             if (latch_d >= 0) {
                 if (reach < 2) ok = false;   // d alone: the fallback rules decide
-                const PuctNodeChild* d = cs + latch_d;
+                const float ds = S.key_s[latch_d], dp = S.key_p[latch_d];
                 for (int i = 0; ok && i < n; ++i) {
                     if (i == latch_d || S.scores[i] == -1e300) continue;
-                    if (selectBefore(cs + i, d, lead)) ++rank;
-                    else if (!selectBefore(d, cs + i, lead)) ok = false;   // tie: position undetermined
+                    const float is = S.key_s[i], ip = S.key_p[i];
+                    const bool i_before = (is < 0 && ds < 0) ? ip > dp : is > ds;
+                    const bool d_before = (ds < 0 && is < 0) ? dp > ip : ds > is;
+                    if (i_before) ++rank;
+                    else if (!d_before) ok = false;   // tie: position undetermined
                 }
+            } else if (!sep_all) {
+                ok = false;
             }
             if (ok) {
                 bool latched = false;
@@ -699,31 +732,14 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
                     if (j == rank && latch_d >= 0 && v > 0.1) latched = true;
                 }
                 if (latched) {
-                    S.scores[latch_d] = -1e300;
-                    best = -1;
-                    for (int i = 0; i < n; ++i) {
-                        if (S.scores[i] == -1e300) continue;
-                        if (best < 0 || S.scores[i] > best_score) {
-                            best = i;
-                            best_score = S.scores[i];
-                        }
-                    }
-                    ok = best >= 0 && best_score > -1.0;
+                    ok = sep_no_d;
+                    best = j1;
+                } else {
+                    ok = sep_all;
                 }
             }
-        }
-        if (ok) {
-            // order independence of `if (score > best_score_float)`: the max m must replace any
-            // incumbent (m > float(c)) and never be replaced (c <= float(m)).
-            const double fm = (float)best_score;
-            for (int i = 0; i < n; ++i) {
-                if (i == best || S.scores[i] == -1e300) continue;
-                const double sc = S.scores[i];
-                if (sc > fm || !(best_score > (double)(float)sc)) {
-                    ok = false;
-                    break;
-                }
-            }
+        } else if (ok) {
+            ok = sep_all;
         }
         if (ok) {
             chosen = chosen_best = cs + best;

@@ -75,6 +75,7 @@ struct gz_runner {
     std::atomic<bool> stop{false};
     std::atomic<long> batches{0}, rows{0}, launches{0}, samples_taken{0}, segments{0};
     std::atomic<long> kernel_us{0}, trunk_us{0};
+    std::atomic<long> engine_idle_us{0};   // summed over engine threads: no pool of the thread ready
     // launches that ran the multi-board trunk variant (rows >= gz_net_large_min_rows)
     std::atomic<long> large_launches{0}, large_rows{0}, large_trunk_us{0};
     int large_min_rows = 1 << 30;
@@ -104,6 +105,9 @@ static void engine_main(gz_runner* r, int tid) {
     for (int k = 0; k < P; ++k) mine.push_back(tid * P + k);
     for (int i : mine) gz_pool_start(r->pools[i].pool, &r->conf);
     int idle = 0;
+    using clk = std::chrono::steady_clock;
+    clk::time_point idle_since{};
+    bool idling = false;
     while (!r->stop.load(std::memory_order_relaxed)) {
         bool progressed = false;
         for (int i : mine) {
@@ -142,6 +146,16 @@ static void engine_main(gz_runner* r, int tid) {
         }
         if (progressed) {
             idle = 0;
+            if (idling) {
+                r->engine_idle_us.fetch_add(
+                    std::chrono::duration_cast<std::chrono::microseconds>(clk::now() - idle_since).count(),
+                    std::memory_order_relaxed);
+                idling = false;
+            }
+        } else if (!idling) {
+            idling = true;
+            idle_since = clk::now();
+            cpu_relax();
         } else if (++idle < 2000) {
             cpu_relax();
         } else {
@@ -375,6 +389,7 @@ extern "C" int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out) {
     out->rows = r->rows.load();
     out->kernel_ms = r->kernel_us.load() / 1000.0;
     out->trunk_ms = r->trunk_us.load() / 1000.0;
+    out->engine_idle_ms = r->engine_idle_us.load() / 1000.0;
     out->large_launches = r->large_launches.load();
     out->large_rows = r->large_rows.load();
     out->large_trunk_ms = r->large_trunk_us.load() / 1000.0;

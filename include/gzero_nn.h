@@ -142,6 +142,7 @@ typedef struct gz_runner_stats {
     long large_launches;         /* launches that ran the two-boards-per-workgroup trunk variant */
     long large_rows;
     double large_trunk_ms;
+    double engine_idle_ms;       /* summed over engine threads: time with none of the thread's pools ready */
 } gz_runner_stats;
 
 gz_runner* gz_runner_create(gz_net* net, const struct gz_sm* sm, const struct gz_transformer* t,
