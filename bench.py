@@ -151,8 +151,11 @@ def main():
     torch.cuda.synchronize()
     net.set_weights_device(blob.data_ptr(), net.weight_count)
 
-    cpus = os.cpu_count() or 4
-    threads = args.threads or max(1, min(14, cpus // max(1, world) - 2))   # + launcher + main
+    # the CPUs this process may run on (the GPU box pins 16 per GPU; os.cpu_count() is the machine)
+    cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 4)
+    if world > 1 and cpus >= (os.cpu_count() or cpus):   # unpinned ranks share the machine
+        cpus = cpus // world
+    threads = args.threads or max(1, min(15, cpus - 1))   # + the launcher (mostly asleep) and main
     runner = SelfPlayRunner(net, sm, transformer, selfplay_conf(args.mode, args.evals), device=local_rank,
                             num_threads=threads, pools_per_thread=args.pools, batch_size=args.batch,
                             seed=args.seed,

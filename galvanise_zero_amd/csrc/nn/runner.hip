@@ -211,7 +211,9 @@ static void launcher_main(gz_runner* r) {
             continue;
         }
         if (inflight.size() >= 2) {
-            cpu_relax();
+            // both launch slots busy: sleep until the older batch completes (blocking-sync event),
+            // leaving the core to the engine threads
+            (void)hipEventSynchronize(r->batches_ring[inflight.front()].ev1);
             continue;
         }
         // gather every waiting pool into one segmented launch
@@ -224,7 +226,7 @@ static void launcher_main(gz_runner* r) {
                 if (inflight.empty())
                     r->qcv.wait_for(lk, std::chrono::microseconds(200));
                 else
-                    r->qcv.wait_for(lk, std::chrono::microseconds(5));
+                    r->qcv.wait_for(lk, std::chrono::microseconds(30));
             }
             while (!r->queue.empty() && (int)b.pools.size() < GZ_MAX_SEGMENTS) {
                 const int i = r->queue.front();
@@ -301,7 +303,7 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
     bool ok = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess;
     for (Batch& b : r->batches_ring)
         ok = ok && hipEventCreate(&b.ev0) == hipSuccess && hipEventCreate(&b.evm) == hipSuccess &&
-             hipEventCreate(&b.ev1) == hipSuccess;
+             hipEventCreateWithFlags(&b.ev1, hipEventBlockingSync) == hipSuccess;
     if (!ok) {
         g_err = "stream / event creation failed";
         gz_runner_destroy(r);
