@@ -184,13 +184,17 @@ private:
 
 }  // namespace
 
+StateMachine* create_more_state_machine(const std::string& name);   // games_more.cpp
+
 StateMachine* create_state_machine(const std::string& name) {
     if (name == "breakthrough") return new Breakthrough(8, "breakthrough", "cellHolds");
     if (name == "breakthroughSmall") return new Breakthrough(6, "breakthroughSmall", "cell");
     if (name == "bt_7") return new Breakthrough(7, "bt_7", "cellHolds");
-    return nullptr;
+    return create_more_state_machine(name);
 }
 
-std::vector<std::string> known_games() { return {"breakthrough", "breakthroughSmall", "bt_7"}; }
+std::vector<std::string> known_games() {
+    return {"breakthrough", "breakthroughSmall", "bt_7", "reversi", "hexLG13", "amazons_10x10"};
+}
 
 }  // namespace gz

@@ -70,7 +70,8 @@ struct KParams {
     const float* vdw;        // value dense [VH][V]
     const float* vdb;        // [V]
     float* feat;             // scratch [n][HC*HW]: head features in flatten order (trunk -> heads)
-    int n;                   // boards in this launch
+    f32x4* resid;            // global-residual variants only: [grid][4 waves][CT*TT][64 lanes]
+    int n;                  // boards in this launch
     int nseg;                // segments (>= 1), ascending row0, seg[0].row0 == 0
     Segment seg[kMaxSegments];
     unsigned long long* stamps;   // diagnostics only (GZ_KERNEL_STAMPS): [grid][8] s_memtime per phase
@@ -81,11 +82,11 @@ struct KParams {
 
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
 
-// ring depth: largest R dividing the stages per conv with R slots of KS*CT fragments <= 96 VGPRs
-__host__ __device__ constexpr int ring_depth(int nst, int ks, int ct) {
+// ring depth: largest R dividing the stages per conv with R slots of KS*CT fragments <= cap VGPRs
+__host__ __device__ constexpr int ring_depth(int nst, int ks, int ct, int cap) {
     const int cand[5] = {9, 6, 4, 3, 2};
     for (int i = 0; i < 5; ++i)
-        if (nst % cand[i] == 0 && cand[i] * ks * ct * 4 <= 96 && (cand[i] - 1) * ks * ct <= 60) return cand[i];
+        if (nst % cand[i] == 0 && cand[i] * ks * ct * 4 <= cap && (cand[i] - 1) * ks * ct <= 60) return cand[i];
     return 1;
 }
 
@@ -99,11 +100,26 @@ struct Geo {
     static constexpr int CPR = F / 8;                // 16-byte chunks of channels per row
     static constexpr int ROWS = ((CPR + 14) * 16 + 255) & ~255;   // LDS row stride (rotated chunks)
     static constexpr int ACT_BYTES = (NPOS + 1) * ROWS;           // + one all-zero row
-    static constexpr int KS = 2;                     // k-steps per ring stage
+    // k-steps per ring stage and the ring's VGPR budget: F = 256 (4 co tiles per wave, 16 weight
+    // VGPRs per k-step) streams single k-steps through a 64-VGPR ring so the accumulators, the
+    // residual and the B fragments still fit the 512 registers of a wave without spilling
+    static constexpr int KS = CT >= 4 ? 1 : 2;
     static constexpr int NST = 9 * KC / KS;          // ring stages per conv
-    static constexpr int R = ring_depth(NST, KS, CT);
+    static constexpr int R = ring_depth(NST, KS, CT, CT >= 4 ? 64 : 96);
     static constexpr int LPS = KS * CT;              // weight loads per stage per lane
+    // Single-image mode: when two ping-pong images (+ bias table) do not fit the 160 KB of LDS
+    // (F = 256 on 10x10 / 13x13 boards), one image is overwritten in place: every conv's MFMAs
+    // finish reading it (barrier) before its epilogue writes it.  The input staging and head
+    // scratch then alias the image.
+    static constexpr bool SI = 2 * NB * ACT_BYTES + 16 * 1024 > 160 * 1024;
+    // Global residual: when the fp32 residual stream (+ the accumulators) would need more than 256
+    // VGPRs (F = 256 on 13x13: 2 x 176), it lives in a per-workgroup device scratch instead of
+    // registers, lane-contiguous (one coalesced 1 KB store / load per wave and tile).
+    static constexpr bool RG = CT * TT * 4 * 2 > 256;
     static_assert(F % 64 == 0, "filters must be a multiple of 64");
+    static_assert(!SI || NB == 1, "single-image mode takes one board per workgroup");
+    static_assert(!RG || SI, "the global residual is implemented for single-image kernels");
+    static constexpr int RESID_BYTES = RG ? 4 * CT * TT * 64 * 16 : 0;   // per workgroup
     static_assert(KC % KS == 0, "a stage must not straddle a tap");
     static_assert(R >= 2, "no ring depth fits");
 };
@@ -184,10 +200,17 @@ struct Ring {
 // Issue stage `gs` of the trunk weight stream (clamped to the last stage) into ring slot SLOT.
 // Fragment (step, ct) of a lane: wres + (step*F + 16ct)*64 bytes + woff, woff = lane's row/slice;
 // the stage base is scalar, ct is the instruction's immediate offset.
+// Single-image (F = 256) kernels run at the 512-register limit, where the register allocator
+// copies values between VGPRs and AGPRs freely: an inline-asm load's destination could be copied
+// (or its register reused) before the data lands.  They issue the ring with ordinary loads, which
+// the compiler tracks (it places the waits and never copies an in-flight register).
 template <int F, int H, int W, int NB, int SLOT, int... CTS>
 __device__ __forceinline__ void ring_issue_k(Ring<F, H, W, NB>& ring, int k, uint32_t woff, const char* sb,
                                              std::integer_sequence<int, CTS...>) {
-    ((ring.r[SLOT][k][CTS] = gload_issue<CTS * 16 * 64>(woff, sb)), ...);
+    if constexpr (Geo<F, H, W, NB>::SI)
+        ((ring.r[SLOT][k][CTS] = *(const bf16x8*)(sb + woff + CTS * 16 * 64)), ...);
+    else
+        ((ring.r[SLOT][k][CTS] = gload_issue<CTS * 16 * 64>(woff, sb)), ...);
 }
 template <int F, int H, int W, int NB, int SLOT>
 __device__ __forceinline__ void ring_issue(Ring<F, H, W, NB>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
@@ -204,6 +227,8 @@ __device__ __forceinline__ void ring_issue(Ring<F, H, W, NB>& ring, const __bf16
 // once per tap so these offsets are computed when the tap starts instead of being hoisted for all
 // nine taps out of the trunk loop, which would pin 9*PT address registers for the whole kernel.
 __device__ __forceinline__ void launder(int& v) { asm volatile("" : "+v"(v)); }
+template <typename T>
+__device__ __forceinline__ void launder_ptr(T*& p) { asm volatile("" : "+v"(p)); }
 template <int F, int H, int W>
 __device__ __forceinline__ int tap_base(int tap, int pt, int lane) {
     using G = Geo<F, H, W>;
@@ -228,11 +253,13 @@ __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, H
     constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC;
     // refill the slot stage ST-1 consumed with stage ST+R-1, then wait for stage ST
     ring_issue<F, H, W, NB, (ST + R - 1) % R>(ring, wres, woff, gs0 + ST + R - 1, gmax);
-    ring_wait<(R - 1) * G::LPS>();
+    if constexpr (!G::SI) {
+        ring_wait<(R - 1) * G::LPS>();
 #pragma unroll
-    for (int k = 0; k < KS; ++k)
+        for (int k = 0; k < KS; ++k)
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) ring_ready(ring.r[ST % R][k][ct]);
+            for (int ct = 0; ct < CT; ++ct) ring_ready(ring.r[ST % R][k][ct]);
+    }
 
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
@@ -302,9 +329,10 @@ trunk_kernel(const KParams kp) {
     constexpr int NPOS = G::NPOS, PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, kThreads = 256;
     constexpr int ACT = G::ACT_BYTES;
 
+    constexpr bool SI = G::SI, RG = G::RG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* X0 = smem;                 // [NB][ACT]
-    char* X1 = smem + NB * ACT;      // [NB][ACT]
+    char* X0 = smem;                           // [NB][ACT]
+    char* X1 = SI ? smem : smem + NB * ACT;    // [NB][ACT]
     char* SCR = X1;                  // scratch aliases X1 while X1 holds no live activations
     float* btab = (float*)(smem + kp.btab_off);   // trunk conv biases [2B][F], after X1 / scratch
 
@@ -326,7 +354,9 @@ trunk_kernel(const KParams kp) {
     if (kp.B > 0) ring_prime<F, H, W, NB>(ring, kp.wres, woff, gmax, std::make_integer_sequence<int, R - 1>{});
 
     f32x4 acc[CT][TT];
-    f32x4 resid[CT][TT];
+    f32x4 resid[RG ? 1 : CT][RG ? 1 : TT];
+    // global residual of this wave: tile (ct, t) at rg[(ct * TT + t) * 64]
+    f32x4* rg = RG ? kp.resid + ((size_t)(blockIdx.x * 4 + wave) * CT * TT) * 64 + lane : nullptr;
 
     for (int i = tid; i < 2 * kp.B * F; i += kThreads) btab[i] = kp.bres[i];
     for (int i = tid; i < NB * G::ROWS / 4; i += kThreads) {
@@ -383,6 +413,7 @@ trunk_kernel(const KParams kp) {
                         __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], bq, acc[ct][bb * PT + pt], 0, 0, 0);
             }
         }
+        if constexpr (SI) __syncthreads();    // the image overwrites the im2col scratch
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -394,7 +425,9 @@ trunk_kernel(const KParams kp) {
                 v[1] = act_fn(v[1] + bias.y, kp.leaky);
                 v[2] = act_fn(v[2] + bias.z, kp.leaky);
                 v[3] = act_fn(v[3] + bias.w, kp.leaky);
-                resid[ct][bb * PT + pt] = v;
+                if constexpr (RG) rg[(ct * TT + bb * PT + pt) * 64] = v;
+                else resid[ct][bb * PT + pt] = v;
+                acc[ct][bb * PT + pt] = v;    // the heads read acc when there is no residual block
                 store_act<F, H, W>(X0 + bb * ACT, 16 * pt + li, co, v);
             }
         }
@@ -408,6 +441,45 @@ trunk_kernel(const KParams kp) {
 
     GZ_STAMP(1);
     // ---- residual tower ------------------------------------------------------------------
+    if constexpr (SI) {
+        // one image, one conv call site (keeps the fully unrolled F = 256 conv once in the binary)
+        for (int cv = 0; cv < 2 * kp.B; ++cv) {
+            const bool second = cv & 1;
+            const float* bt = btab + cv * F;
+            conv3x3<F, H, W, NB>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane);
+            __syncthreads();    // every wave has finished reading the image it is about to overwrite
+            // residual tile addresses are formed here, not hoisted out of the loop (44 x 64-bit)
+            f32x4* rgc = rg;
+            if constexpr (RG) launder_ptr(rgc);
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const int co = co_base + 16 * ct + 4 * g;
+                const float4 bias = *(const float4*)(bt + co);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    f32x4 v = acc[ct][t];
+                    v[0] += bias.x; v[1] += bias.y; v[2] += bias.z; v[3] += bias.w;
+                    if (second) {
+                        f32x4 r;
+                        if constexpr (RG) r = rgc[(ct * TT + t) * 64];
+                        else r = resid[ct][t];
+                        v[0] += r[0]; v[1] += r[1]; v[2] += r[2]; v[3] += r[3];
+                    }
+                    v[0] = act_fn(v[0], kp.leaky);
+                    v[1] = act_fn(v[1], kp.leaky);
+                    v[2] = act_fn(v[2], kp.leaky);
+                    v[3] = act_fn(v[3], kp.leaky);
+                    if (second) {
+                        if constexpr (RG) rgc[(ct * TT + t) * 64] = v;
+                        else resid[ct][t] = v;
+                        acc[ct][t] = v;
+                    }
+                    store_act<F, H, W>(X0, 16 * t + li, co, v);
+                }
+            }
+            __syncthreads();
+        }
+    } else
     for (int blk = 0; blk < kp.B; ++blk) {
         const float* b_a = btab + (2 * blk) * F;
         const float* b_b = b_a + F;
@@ -443,13 +515,14 @@ trunk_kernel(const KParams kp) {
                 v[2] = act_fn(v[2] + bias.z + r[2], kp.leaky);
                 v[3] = act_fn(v[3] + bias.w + r[3], kp.leaky);
                 resid[ct][t] = v;
+                acc[ct][t] = v;
                 store_act<F, H, W>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v);
             }
         }
         __syncthreads();
     }
     // the clamped tail stages are never consumed: land them before their registers are released
-    if (kp.B > 0) {
+    if (!SI && kp.B > 0) {
         ring_wait<0>();
 #pragma unroll
         for (int s = 0; s < R; ++s)
@@ -460,7 +533,8 @@ trunk_kernel(const KParams kp) {
     }
 
     GZ_STAMP(2);
-    // ---- the heads' 1x1 convs (2 per policy role + 1 value) from the fp32 residual registers;
+    // ---- the heads' 1x1 convs (2 per policy role + 1 value) from the fp32 residual stream (a copy
+    // of the last epilogue's output is in acc);
     // features in the model's Flatten order go to the scratch for heads_kernel ----------------
     const int HC = 2 * kp.R + 1;
     float* hpart = (float*)SCR;                                  // [4][HC][NPOS]
@@ -480,7 +554,7 @@ trunk_kernel(const KParams kp) {
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) s += resid[ct][bb * PT + pt][r] * wv[ct][r];
+                    for (int r = 0; r < 4; ++r) s += acc[ct][bb * PT + pt][r] * wv[ct][r];
                 s += __shfl_xor(s, 16, 64);
                 s += __shfl_xor(s, 32, 64);
                 const int p = 16 * pt + li;

@@ -43,6 +43,7 @@ struct gz_net {
         int nb = 1;                // boards per workgroup
         int smem = 0;              // dynamic LDS bytes
         int btab_off = 0;          // LDS offset of the bias table
+        int resid_bytes = 0;       // global residual scratch per workgroup
     } small, large;                // launches below / from large_min_rows rows
     int large_min_rows = 1 << 30;
     bool has_weights = false;
@@ -58,6 +59,7 @@ struct gz_net {
     int heads_smem = 0;
     std::mutex feat_mu;            // head-feature scratch, one per stream (launches on one stream are ordered)
     std::map<hipStream_t, std::pair<float*, int>> feat;
+    std::map<hipStream_t, std::pair<char*, size_t>> resid;   // global-residual scratch per stream
     unsigned long long* d_stamps = nullptr;   // GZ_KERNEL_STAMPS diagnostics
     int stamp_cap = 0;
     bool stamps_on = false;
@@ -75,6 +77,8 @@ struct KernelChoice {
     const void* fn = nullptr;
     int act_bytes = 0;
     int nb = 1;
+    bool single_image = false;
+    int resid_bytes = 0;           // global residual scratch per workgroup (0: registers)
 };
 
 template <int F, int H, int W, int NB, int WPE>
@@ -83,12 +87,16 @@ static KernelChoice kernel_for() {
     k.fn = (const void*)&trunk_kernel<F, H, W, NB, WPE>;
     k.act_bytes = Geo<F, H, W, NB>::ACT_BYTES;
     k.nb = NB;
+    k.single_image = Geo<F, H, W, NB>::SI;
+    k.resid_bytes = Geo<F, H, W, NB>::RESID_BYTES;
     return k;
 }
 
 template <int F, int H, int W>
 static KernelChoice variants(int v) {
-    switch (v) {
+    if constexpr (4 * Geo<F, H, W, 1>::ACT_BYTES + 16 * 1024 > 160 * 1024) {   // large boards / filters: one board per workgroup only
+        return v == 11 ? kernel_for<F, H, W, 1, 1>() : KernelChoice{};
+    } else switch (v) {
         case 11: return kernel_for<F, H, W, 1, 1>();
         case 12: return kernel_for<F, H, W, 1, 2>();
         case 21: return kernel_for<F, H, W, 2, 1>();
@@ -110,6 +118,8 @@ static KernelChoice select_kernel(int F, int H, int W, int v) {
     GZ_CASE(128, 6, 6)
     GZ_CASE(64, 8, 8)
     GZ_CASE(128, 8, 8)
+    GZ_CASE(256, 10, 10)
+    GZ_CASE(256, 13, 13)
 #undef GZ_CASE
     return KernelChoice{};
 }
@@ -145,7 +155,11 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         min_large = 1 << 30;
     }
     const KernelChoice kc = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vs);
-    const KernelChoice kl = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vl);
+    KernelChoice kl = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vl);
+    if (kc.fn && !kl.fn && vl != vs) {   // geometries with a single (one board per workgroup) variant
+        kl = kc;
+        min_large = 1 << 30;
+    }
     if (!kc.fn || !kl.fn) {
         fail("unsupported network geometry F=" + std::to_string(d.cnn_filter_size) + " H=" +
              std::to_string(d.input_columns) + " W=" + std::to_string(d.input_rows));
@@ -167,7 +181,9 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         gz_net::Trunk t;
         t.fn = c.fn;
         t.nb = c.nb;
-        t.btab_off = c.nb * c.act_bytes + std::max(c.nb * c.act_bytes, scr);
+        t.btab_off = c.single_image ? align16(std::max(c.act_bytes, scr))
+                                    : c.nb * c.act_bytes + std::max(c.nb * c.act_bytes, scr);
+        t.resid_bytes = c.resid_bytes;
         t.smem = t.btab_off + bias_table_bytes(d.cnn_filter_size, d.residual_layers);
         return t;
     };
@@ -194,6 +210,11 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         return nullptr;
     }
     for (const gz_net::Trunk* t : {&net->small, &net->large}) {
+        if (t->smem > 160 * 1024) {
+            fail("network needs " + std::to_string(t->smem) + " B of LDS per workgroup (160 KB max)");
+            delete net;
+            return nullptr;
+        }
         if (t->smem > 64 * 1024 &&
             hipFuncSetAttribute(t->fn, hipFuncAttributeMaxDynamicSharedMemorySize, t->smem) != hipSuccess) {
             fail("cannot raise dynamic LDS limit");
@@ -218,6 +239,7 @@ extern "C" void gz_net_destroy(gz_net* net) {
     if (net->d_io) (void)hipFree(net->d_io);
     if (net->d_stamps) (void)hipFree(net->d_stamps);
     for (auto& f : net->feat) (void)hipFree(f.second.first);
+    for (auto& f : net->resid) (void)hipFree(f.second.first);
     if (net->ev0) (void)hipEventDestroy(net->ev0);
     if (net->ev1) (void)hipEventDestroy(net->ev1);
     if (net->stream) (void)hipStreamDestroy(net->stream);
@@ -425,6 +447,23 @@ static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* se
         kp.feat = f.first;
     }
     const gz_net::Trunk& t = n >= net->large_min_rows ? net->large : net->small;
+    kp.resid = nullptr;
+    if (t.resid_bytes) {
+        std::lock_guard<std::mutex> lk(net->feat_mu);
+        auto& f = net->resid[stream];
+        const size_t need = (size_t)((n + t.nb - 1) / t.nb) * t.resid_bytes;
+        if (f.second < need) {
+            if (f.first) {
+                HIPCHK(hipDeviceSynchronize());
+                HIPCHK(hipFree(f.first));
+                f.first = nullptr;
+            }
+            const size_t cap = std::max(need, (size_t)1024 * t.resid_bytes);
+            HIPCHK(hipMalloc((void**)&f.first, cap));
+            f.second = cap;
+        }
+        kp.resid = (f32x4*)f.first;
+    }
     kp.btab_off = t.btab_off;
     void* args[] = {&kp};
     HIPCHK(hipLaunchKernel(t.fn, dim3((n + t.nb - 1) / t.nb), dim3(256), args, t.smem, stream));

@@ -66,6 +66,27 @@ class Games(object):
                         [simple_board_channels("cell", ["white", "black"])],
                         [binary_control("control", "white", "black")])
 
+    def reversi(self):
+        # gamedesc.py:152-160: cell {black, red}; control black -> 0, red -> 1
+        return GameDesc("reversi", _cords(8), _cords(8),
+                        [simple_board_channels("cell", ["black", "red"])],
+                        [binary_control("control", "black", "red")])
+
+    def hexLG13(self):
+        # gamedesc.py:309-318: x = row letters a..m, y = numbers 1..13; control black -> 0, white -> 1
+        return GameDesc("hex", list("abcdefghijklm"), _cords(13),
+                        [simple_board_channels("cell", ["black", "white"])],
+                        [binary_control("control", "black", "white")])
+
+    def amazons_10x10(self):
+        # gamedesc.py:216-232: justMoved plane + cell {white, black, arrow}; four turn planes
+        controls = [simple_control("turn", "black", "move"), simple_control("turn", "black", "fire"),
+                    simple_control("turn", "white", "move"), simple_control("turn", "white", "fire")]
+        return GameDesc("amazons_10x10", _cords(10), _cords(10),
+                        [BoardChannels("justMoved", 1, 2),
+                         simple_board_channels("cell", ["white", "black", "arrow"])],
+                        controls)
+
     def bt_7(self):
         return GameDesc("breakthrough", _cords(7), _cords(7),
                         [simple_board_channels("cellHolds", ["white", "black"])],

@@ -13,14 +13,19 @@ from oracle import games_ref
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.mark.parametrize("game", ["breakthrough", "breakthroughSmall"])
+ALL_GAMES = ["breakthrough", "breakthroughSmall", "reversi", "hexLG13", "amazons_10x10"]
+# playouts per game: the pure-Python oracles of the larger games are slow
+PLAYOUTS = {"breakthrough": 60, "breakthroughSmall": 60, "reversi": 30, "hexLG13": 12, "amazons_10x10": 6}
+
+
+@pytest.mark.parametrize("game", ALL_GAMES)
 def test_policy_sizes_match_reference_models(game):
     arch = json.load(open(os.path.join(GOLDEN, "arch.json")))
     sm = get_sm(game)
     assert [sm.action_count(r) for r in range(sm.role_count)] == arch[game]["policy_units"]
 
 
-@pytest.mark.parametrize("game", ["breakthrough", "breakthroughSmall"])
+@pytest.mark.parametrize("game", ALL_GAMES)
 def test_random_playouts_match_oracle(game):
     sm = get_sm(game)
     ref = games_ref.make(game)
@@ -29,11 +34,11 @@ def test_random_playouts_match_oracle(game):
         assert sm.base_name(i) == ref.base_name(i)
     rng = np.random.default_rng(123)
     games = 0
-    for g in range(60):
+    for g in range(PLAYOUTS[game]):
         words = sm.get_initial_state()
         s = ref.initial_state
         assert games_ref.words_to_state(words) == s
-        for depth in range(400):
+        for depth in range(1000):
             sm.update_bases(words)
             assert sm.is_terminal() == ref.is_terminal(s)
             if sm.is_terminal():
@@ -49,7 +54,7 @@ def test_random_playouts_match_oracle(game):
             words = sm.next_state(joint)
             s = ref.next_state(s, joint)
             assert games_ref.words_to_state(words) == s
-    assert games == 60
+    assert games == PLAYOUTS[game]
 
 
 def test_breakthrough_initial_moves():

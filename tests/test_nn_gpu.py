@@ -30,12 +30,21 @@ VARIANTS = {
     "b0_8x8": NetDesc(5, 8, 8, 128, 0, [155, 155]),
     "leaky_v3_8x8": NetDesc(5, 8, 8, 64, 1, [65, 65], num_values=3, leaky_relu=True),
     "nchw_6x6": NetDesc(5, 6, 6, 128, 1, [81, 81], flatten_nchw=True),
+    # BASELINE configs 3-5 (reversi 8x8 with the draw head; F = 256 nets on 13x13 / 10x10 boards,
+    # the single-LDS-image kernels, 13x13 with the residual stream in a device scratch)
+    "cfg3": BASELINE_CONFIGS[3]["desc"],
+    "cfg4": BASELINE_CONFIGS[4]["desc"],
+    "cfg5": BASELINE_CONFIGS[5]["desc"],
+    "b2_13x13_f256": NetDesc(5, 13, 13, 256, 2, [170, 171], flatten_nchw=True),
+    "b0_10x10_f256_v3": NetDesc(12, 10, 10, 256, 0, [3041, 3041], num_values=3, leaky_relu=True),
 }
+DEEP = {"cfg3", "cfg4", "cfg5"}       # residual gamma damped so the softmaxes do not saturate
+BIG = {"cfg4", "cfg5", "b2_13x13_f256", "b0_10x10_f256_v3"}   # oracle batch sizes kept small
 
 
-def _net(desc, seed, device):
+def _net(desc, seed, device, name=None):
     from galvanise_zero_amd._native import HipNet
-    w = random_weights(desc, seed, bias_std=0.2)
+    w = random_weights(desc, seed, bias_std=0.2, res_gamma=0.15 if name in DEEP else 1.0)
     net = HipNet(desc, device)
     net.set_weights(to_blob(w))
     return net, w
@@ -49,9 +58,9 @@ def _err(a, b):
 @pytest.mark.parametrize("name", list(VARIANTS))
 def test_forward_parity(name, hip_device):
     desc = VARIANTS[name]
-    net, w = _net(desc, 7919, hip_device)
+    net, w = _net(desc, 7919, hip_device, name)
     tol_emu = TOL_EMU_SHALLOW if desc.residual_layers <= 1 else TOL_EMU_DEEP
-    for n in (1, 7, 64):
+    for n in ((1, 7, 19) if name in BIG else (1, 7, 64)):
         x = random_planes(desc, n, 100 + n)
         got = net.forward(x)
         ref = nn_ref.forward(desc, w, x)
@@ -67,10 +76,10 @@ def test_forward_parity(name, hip_device):
             np.testing.assert_allclose(g.sum(axis=1), 1.0, atol=1e-4)
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg5"])
 def test_batch_invariance(name, hip_device):
     desc = VARIANTS[name]
-    net, _ = _net(desc, 3, hip_device)
+    net, _ = _net(desc, 3, hip_device, name)
     x = random_planes(desc, 256, 9)
     full = net.forward(x)
     # same rows in a different batch composition / slot
