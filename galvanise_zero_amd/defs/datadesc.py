@@ -1,8 +1,14 @@
 """Data records of the hot path: Sample (reference src/ggpzero/defs/datadesc.py:8-38, the dict
-layout sampleToDict emits, supervisor_impl.cpp:75-118) and GenerationDescription (datadesc.py:60-100)."""
+layout sampleToDict emits, supervisor_impl.cpp:75-118), GenerationSamples (datadesc.py:40-52) and
+GenerationDescription (datadesc.py:55-95)."""
 import attr
 
+from ..util.attrutil import register_attrs
 
+_WIRE = "ggpzero.defs.datadesc"     # module name in the reference's JSON class tags
+
+
+@register_attrs(_WIRE)
 @attr.s
 class Sample(object):
     state = attr.ib(default=attr.Factory(list))
@@ -19,6 +25,18 @@ class Sample(object):
     resultant_puct_visits = attr.ib(default=0)
 
 
+@register_attrs(_WIRE)
+@attr.s
+class GenerationSamples(object):
+    """datadesc.py:40-52: one gendata_<game>_<step>.json.gz file."""
+    game = attr.ib(default="game")
+    date_created = attr.ib(default="2018-01-24 22:28")
+    with_generation = attr.ib(default="v6_123")
+    num_samples = attr.ib(default=1024)
+    samples = attr.ib(default=attr.Factory(list))
+
+
+@register_attrs(_WIRE)
 @attr.s
 class GenerationDescription(object):
     game = attr.ib(default="breakthrough")
