@@ -47,7 +47,10 @@ def parse():
     ap.add_argument("--threads", type=int, default=0, help="host threads per GPU (0: auto)")
     ap.add_argument("--pools", type=int, default=4, help="game pools per thread")
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--evals", type=int, default=800)
+    ap.add_argument("--evals", type=int, default=0, help="evals per move (0: the config's, 800 for cfg2)")
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
+                    help="BASELINE.json configs[i-1]; 2 (breakthrough 8x8, 6x128) is the headline workload, "
+                         "3-5 (reversi 10x128, hexLG13 12x256, amazons_10x10 20x256) run the same path")
     ap.add_argument("--mode", choices=["template", "literal"], default="template")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -66,22 +69,25 @@ def selfplay_conf(mode, evals):
     return conf
 
 
-def setup_game():
+def setup_game(config=2):
     from galvanise_zero_amd.defs import templates
     from galvanise_zero_amd.nn.bases import GdlBasesTransformer
     from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS
     from galvanise_zero_amd.sm import get_sm
-    cfg = BASELINE_CONFIGS[2]
+    cfg = BASELINE_CONFIGS[config]
     sm = get_sm(cfg["game"])
-    gen = templates.default_generation_desc(cfg["game"], num_previous_states=1)
+    gen = templates.default_generation_desc(cfg["game"], num_previous_states=1,
+                                            draw_head=cfg["desc"].num_values == 3)
     transformer = GdlBasesTransformer(sm, gen)
     desc = cfg["desc"]
     assert (transformer.num_channels, transformer.num_cols, transformer.num_rows) == \
         (desc.input_channels, desc.input_columns, desc.input_rows)
+    assert list(transformer.policy_dist_count) == list(desc.policy_dist_count)
+    assert transformer.num_rewards == desc.num_values
     return sm, transformer, desc
 
 
-def cpu_baseline(seconds, evals, mode, batch):
+def cpu_baseline(seconds, evals, mode, batch, config=2):
     """CPU restatement timed on the host: the same engine driven by the reference's Python poll
     loop with the oracle's CPU forward (oracle/nn_ref.py) in place of the GPU."""
     import numpy as np
@@ -90,7 +96,7 @@ def cpu_baseline(seconds, evals, mode, batch):
     from galvanise_zero_amd.nn.weights import random_weights
     from oracle import nn_ref
 
-    sm, transformer, desc = setup_game()
+    sm, transformer, desc = setup_game(config)
     weights = random_weights(desc, 7921)
     cores = min(16, os.cpu_count() or 1)
 
@@ -116,9 +122,9 @@ def cpu_baseline(seconds, evals, mode, batch):
         el = time.time() - t0
         rows = sup.total_predictions - rows0
     return {"value": rows / el, "unit": "leaf-evals/s", "cores": cores, "kind": "port",
-            "sample": "%.1f s of breakthrough self-play (%d games inline, batch %d, %d evals/move, %s mode): "
+            "sample": "%.1f s of %s self-play (%d games inline, batch %d, %d evals/move, %s mode): "
                       "native engine + oracle fp64 numpy forward via the Python poll loop" %
-                      (el, batch, batch, evals, mode)}
+                      (el, sm.game, batch, batch, evals, mode)}
 
 
 def main():
@@ -140,7 +146,9 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    sm, transformer, desc = setup_game()
+    from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS
+    evals = args.evals or BASELINE_CONFIGS[args.config]["evals"]
+    sm, transformer, desc = setup_game(args.config)
     net = HipNet(desc, local_rank)
 
     # weights: rank 0 creates, RCCL broadcast of the blob (the only collective on the path)
@@ -156,7 +164,7 @@ def main():
     if world > 1 and cpus >= (os.cpu_count() or cpus):   # unpinned ranks share the machine
         cpus = cpus // world
     threads = args.threads or max(1, min(15, cpus - 1))   # + the launcher (mostly asleep) and main
-    runner = SelfPlayRunner(net, sm, transformer, selfplay_conf(args.mode, args.evals), device=local_rank,
+    runner = SelfPlayRunner(net, sm, transformer, selfplay_conf(args.mode, evals), device=local_rank,
                             num_threads=threads, pools_per_thread=args.pools, batch_size=args.batch,
                             seed=args.seed,
                             game_index_base=shard.game_index_base(rank, threads * args.pools * args.batch),
@@ -205,9 +213,10 @@ def main():
         rows_per_launch = rows / launches if launches else float("nan")
         # the trunk kernel runs as one of two variants by launch size; the roofline is reported for
         # the variant that took more trunk time, the other one alongside
+        geo = (desc.cnn_filter_size, desc.input_columns, desc.input_rows)
         variants = {
-            "gznn::trunk_kernel<128, 8, 8, 2, 1>": (l_launches, l_rows, l_tms),
-            "gznn::trunk_kernel<128, 8, 8, 1, 1>": (launches - l_launches, rows - l_rows, tms - l_tms),
+            "gznn::trunk_kernel<%d, %d, %d, 2, 1>" % geo: (l_launches, l_rows, l_tms),
+            "gznn::trunk_kernel<%d, %d, %d, 1, 1>" % geo: (launches - l_launches, rows - l_rows, tms - l_tms),
         }
         per_variant = {}
         for name, (vl, vr, vt) in variants.items():
@@ -235,14 +244,15 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic: self-play from the initial position, random-init weights (no .h5 in reference)",
-            "config": {"workload": "breakthrough 8x8 self-play, v1 6x128 net, %d evals/move (%s mode), eval "
-                                   "batch %d" % (args.evals, args.mode, args.batch),
+            "config": {"workload": "%s self-play (BASELINE configs[%d]), v1 %dx%d net, %d evals/move (%s mode), "
+                                   "eval batch %d" % (sm.game, args.config - 1, desc.residual_layers,
+                                                      desc.cnn_filter_size, evals, args.mode, args.batch),
                        "games_per_gpu": npools * args.batch, "threads_per_gpu": threads,
                        "pools_per_thread": args.pools, "eval_batch": args.batch, "parallelism": "games sharded dp%d" % world},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_BF16_TFLOPS, "traffic": TRAFFIC_PER_LAUNCH.get(dom),
                          "traffic_unit": "bytes/launch",
-                         "traffic_source": TRAFFIC_SOURCE,
+                         "traffic_source": TRAFFIC_SOURCE if dom in TRAFFIC_PER_LAUNCH else None,
                          "kernel": dom, "avg_kernel_ms": per_variant[dom]["avg_kernel_ms"] if dom else None,
                          "rows_per_launch": per_variant[dom]["rows_per_launch"] if dom else None,
                          "flop_per_leaf_kernel": desc.flops_trunk(), "variants": per_variant,
@@ -256,7 +266,7 @@ def main():
             "host_peak_rss_gb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6,
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, args.evals, args.mode, args.batch)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, evals, args.mode, args.batch, args.config)
         print(json.dumps(out), flush=True)
     runner.close()
     if world > 1:

@@ -8,15 +8,36 @@
 """
 import numpy as np
 
-# gamedesc.py:142-150, 169-175: (board base term, piece terms, x/y term idx, piece term idx,
-# coords, control channels [[(args, value), ...], ...])
+# Per-game descriptions restated from src/ggpzero/defs/gamedesc.py (helpers :116-134):
+#   x/y coords (gamedesc GameDesc.x_cords / y_cords), board channels as
+#   (base term, x term idx, y term idx, piece term idx or None, pieces) (BoardChannels / BoardTerm),
+#   control channels as [[(arg terms, value), ...], ...] (ControlChannel / ControlBase).
+_C8 = [str(i) for i in range(1, 9)]
+
+
+def _binary(base, a, b):            # gamedesc.py:120-122
+    return [((base, a), 0), ((base, b), 1)]
+
+
 GAME_DESCS = {
-    "breakthrough": dict(base_term="cellHolds", pieces=["white", "black"], x_idx=1, y_idx=2, piece_idx=3,
-                         coords=[str(i) for i in range(1, 9)],
-                         controls=[[(("control", "black"), 0), (("control", "white"), 1)]]),
-    "breakthroughSmall": dict(base_term="cell", pieces=["white", "black"], x_idx=1, y_idx=2, piece_idx=3,
-                              coords=[str(i) for i in range(1, 7)],
-                              controls=[[(("control", "white"), 0), (("control", "black"), 1)]]),
+    # gamedesc.py:142-150
+    "breakthrough": dict(x=_C8, y=_C8, board=[("cellHolds", 1, 2, 3, ["white", "black"])],
+                         controls=[_binary("control", "black", "white")]),
+    # gamedesc.py:169-175
+    "breakthroughSmall": dict(x=_C8[:6], y=_C8[:6], board=[("cell", 1, 2, 3, ["white", "black"])],
+                              controls=[_binary("control", "white", "black")]),
+    # gamedesc.py:152-160
+    "reversi": dict(x=_C8, y=_C8, board=[("cell", 1, 2, 3, ["black", "red"])],
+                    controls=[_binary("control", "black", "red")]),
+    # gamedesc.py:309-318
+    "hexLG13": dict(x=list("abcdefghijklm"), y=[str(i) for i in range(1, 14)],
+                    board=[("cell", 1, 2, 3, ["black", "white"])],
+                    controls=[_binary("control", "black", "white")]),
+    # gamedesc.py:214-232 (simple_control = one base, value 1)
+    "amazons_10x10": dict(x=[str(i) for i in range(1, 11)], y=[str(i) for i in range(1, 11)],
+                          board=[("justMoved", 1, 2, None, None), ("cell", 1, 2, 3, ["white", "black", "arrow"])],
+                          controls=[[(("turn", "black", "move"), 1)], [(("turn", "black", "fire"), 1)],
+                                    [(("turn", "white", "move"), 1)], [(("turn", "white", "fire"), 1)]]),
 }
 
 
@@ -25,17 +46,24 @@ class Planes(object):
         d = GAME_DESCS[game]
         self.num_prev_states = num_prev_states
         terms = [n.strip("()").split() for n in base_names]
-        self.W = len(d["coords"])          # num_rows = len(x_cords)
-        self.H = len(d["coords"])          # num_cols = len(y_cords)
+        self.W = len(d["x"])               # num_rows = len(x_cords)   (bases.py:104-121)
+        self.H = len(d["y"])               # num_cols = len(y_cords)
         self.channel_size = self.W * self.H
         board, mapping, used = [], {}, set()
+        # bases.py:168-213 create_board_space: first board channel whose base term matches; the
+        # channel key is (base term, matched piece terms), numbered in first-seen base order
         for idx, t in enumerate(terms):
-            if t[0] != d["base_term"] or t[d["piece_idx"]] not in d["pieces"]:
+            bc = next((b for b in d["board"] if b[0] == t[0]), None)
+            if bc is None:
                 continue
-            key = (t[0], t[d["piece_idx"]])
+            base, xi, yi, pi, pieces = bc
+            if pi is not None and t[pi] not in pieces:
+                continue
+            key = (t[0],) if pi is None else (t[0], t[pi])
             mapping.setdefault(key, len(mapping))
-            x = d["coords"].index(t[d["x_idx"]])
-            y = d["coords"].index(t[d["y_idx"]])
+            x = d["x"].index(t[xi])
+            y = d["y"].index(t[yi])
+            # cppinterface.py:44: channel_size * channel_id + y_idx * num_rows + x_idx
             board.append((idx, self.channel_size * mapping[key] + y * self.W + x))
             used.add(idx)
         self.board = board

@@ -10,7 +10,8 @@ from galvanise_zero_amd.sm import get_sm
 from oracle import games_ref, planes_ref
 
 
-@pytest.mark.parametrize("game,prev", [("breakthrough", 1), ("breakthroughSmall", 1), ("breakthrough", 0)])
+@pytest.mark.parametrize("game,prev", [("breakthrough", 1), ("breakthroughSmall", 1), ("breakthrough", 0),
+                                       ("reversi", 1), ("hexLG13", 1), ("amazons_10x10", 1), ("amazons_10x10", 0)])
 def test_planes_match_oracle(game, prev):
     sm = get_sm(game)
     t = GdlBasesTransformer(sm, templates.default_generation_desc(game, num_previous_states=prev))

@@ -174,3 +174,28 @@ def test_player_root_latch_bit_exact():
                                       think_time=-1, converged_visits=1)
     visits = _player_run(setup, conf, 1400, 2, seed=13)
     assert sum(t for _, t, _ in visits[0]) > 1000
+
+
+@pytest.mark.parametrize("game,polls,evals", [("reversi", 2500, 12), ("hexLG13", 300, 8), ("amazons_10x10", 120, 6)])
+def test_supervisor_selfplay_parity_other_games(game, polls, evals):
+    """reversi (3-value draw head, pass moves), hexLG13 (policy heads 170/171), amazons_10x10
+    (12 planes, 3041 moves, 4 turn planes): every batch of planes and every sample bit-identical
+    between the native engine and the oracle restatement."""
+    setup = Setup(game, draw_head=(game == "reversi"))
+    conf = _selfplay_conf(evals, 0.25, True, -1)
+    conf.run_to_end_evals = 4
+    nlog, nsamples, _, _ = run_native_supervisor(setup, conf, 4, polls, seed=11)
+    olog, osamples, _ = run_oracle_supervisor(setup, conf, 4, polls, seed=11, native_log=nlog)
+    assert len(nlog) == len(olog) == polls
+    assert [sample_key(setup, s, True) for s in nsamples] == [sample_key(setup, s, False) for s in osamples]
+    if game == "reversi":
+        assert len(nsamples) > 0
+
+
+@pytest.mark.parametrize("game,evals", [("reversi", 40), ("hexLG13", 30), ("amazons_10x10", 20)])
+def test_player_visit_counts_bit_exact_other_games(game, evals):
+    setup = Setup(game, draw_head=(game == "reversi"))
+    conf = templates.base_puct_config(batch_size=4, choose="choose_temperature", dirichlet_noise_pct=0.25,
+                                      think_time=-1, converged_visits=1)
+    visits = _player_run(setup, conf, evals, 3, seed=13)
+    assert sum(t for _, t, _ in visits[0]) > evals // 2
