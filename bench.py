@@ -250,9 +250,9 @@ def main():
                        "games_per_gpu": npools * args.batch, "threads_per_gpu": threads,
                        "pools_per_thread": args.pools, "eval_batch": args.batch, "parallelism": "games sharded dp%d" % world},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": TRAFFIC_PER_LAUNCH.get(dom),
+                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": TRAFFIC_PER_LAUNCH.get(dom) if args.config == 2 else None,
                          "traffic_unit": "bytes/launch",
-                         "traffic_source": TRAFFIC_SOURCE if dom in TRAFFIC_PER_LAUNCH else None,
+                         "traffic_source": TRAFFIC_SOURCE if args.config == 2 and dom in TRAFFIC_PER_LAUNCH else None,
                          "kernel": dom, "avg_kernel_ms": per_variant[dom]["avg_kernel_ms"] if dom else None,
                          "rows_per_launch": per_variant[dom]["rows_per_launch"] if dom else None,
                          "flop_per_leaf_kernel": desc.flops_trunk(), "variants": per_variant,
