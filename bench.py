@@ -30,6 +30,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0      # gfx950 dense bf16 MFMA (MI355X_MICROARCH.md)
+# L2-served read rate per CU (MI355X_MICROARCH.md "Indexed rows: gather into LDS": rows shared by
+# every workgroup, 66-73 GB/s per CU, 16.8-18.8 TB/s chip-wide).  Every trunk workgroup streams the
+# whole conv weight image from its XCD's L2, so below ~1.5 boards per CU the trunk is bound by this
+# rate, not by the MFMA peak.
+PEAK_L2_GBPS_PER_CU = 70.0
+NUM_CUS = 256
 # PMC-measured fabric bytes per trunk launch (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE,
 # separate rocprofv3 --pmc passes of tools/profile_bench.sh at 256 / 512 rows, profiles/r01d_pmc.txt).
 # PMC counters cannot be read inside the timed run, so the measured per-launch figure of the same
@@ -224,6 +230,16 @@ def main():
                 per_variant[name] = {"launches": vl, "rows_per_launch": vr / vl, "avg_kernel_ms": vt / vl,
                                      "achieved_tflops": desc.flops_trunk() * vr / (vt / 1e3) / 1e12}
         dom = max(per_variant, key=lambda k: variants[k][2]) if per_variant else None
+        # weight stream per trunk workgroup: bf16 3x3 conv weights of every residual conv
+        wbytes = 2 * desc.residual_layers * 9 * desc.cnn_filter_size ** 2 * 2
+        for name, pv in per_variant.items():
+            nb = 2 if name.endswith("2, 1>") else 1
+            wg = pv["rows_per_launch"] / nb
+            cus = min(wg, NUM_CUS)
+            rate = wg * wbytes / (pv["avg_kernel_ms"] / 1e3) / cus / 1e9
+            pv["l2_weight_stream"] = {"bytes_per_workgroup": wbytes, "workgroups_per_launch": wg,
+                                      "achieved_GBps_per_cu": rate, "peak_GBps_per_cu": PEAK_L2_GBPS_PER_CU,
+                                      "frac": rate / PEAK_L2_GBPS_PER_CU}
         achieved = per_variant[dom]["achieved_tflops"] if dom else float("nan")
         out = {
             "metric": "self-play games/sec + NN leaf-evals/sec, breakthrough 8x8 @ 800 playouts/move",
@@ -265,6 +281,8 @@ def main():
             "engine_idle_frac": (idle_ms / 1e3) / (T * world * threads) if T > 0 else None,
             "host_peak_rss_gb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6,
         }
+        if dom:
+            out["roofline"]["l2_weight_stream"] = per_variant[dom]["l2_weight_stream"]
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, evals, args.mode, args.batch, args.config)
         print(json.dumps(out), flush=True)
