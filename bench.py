@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--min-launch-rows", type=int, default=1024,
+                    help="hold a launch (while one is in flight) until this many rows are queued ...")
+    ap.add_argument("--max-launch-wait-us", type=int, default=3000, help="... or its oldest pool waited this long")
     ap.add_argument("--spin-yield", type=int, default=1000,
                     help="yield a game's coroutine after this many NN-free playouts (0: reference behaviour)")
     return ap.parse_args()
@@ -174,7 +177,8 @@ def main():
                             num_threads=threads, pools_per_thread=args.pools, batch_size=args.batch,
                             seed=args.seed,
                             game_index_base=shard.game_index_base(rank, threads * args.pools * args.batch),
-                            spin_yield_playouts=args.spin_yield)
+                            spin_yield_playouts=args.spin_yield, min_launch_rows=args.min_launch_rows,
+                            max_launch_wait_us=args.max_launch_wait_us)
     npools = runner.num_pools
 
     def barrier():
@@ -264,7 +268,8 @@ def main():
                                    "eval batch %d" % (sm.game, args.config - 1, desc.residual_layers,
                                                       desc.cnn_filter_size, evals, args.mode, args.batch),
                        "games_per_gpu": npools * args.batch, "threads_per_gpu": threads,
-                       "pools_per_thread": args.pools, "eval_batch": args.batch, "parallelism": "games sharded dp%d" % world},
+                       "pools_per_thread": args.pools, "eval_batch": args.batch,
+                       "launch_batching": {"min_rows": args.min_launch_rows, "max_wait_us": args.max_launch_wait_us}, "parallelism": "games sharded dp%d" % world},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_BF16_TFLOPS, "traffic": TRAFFIC_PER_LAUNCH.get(dom) if args.config == 2 else None,
                          "traffic_unit": "bytes/launch",

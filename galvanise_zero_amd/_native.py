@@ -364,7 +364,8 @@ class GzRunnerConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("num_threads", ctypes.c_int), ("pools_per_thread", ctypes.c_int),
                 ("batch_size", ctypes.c_int), ("seed", ctypes.c_ulonglong), ("game_index_base", ctypes.c_long),
                 ("per_pool_unique_states", ctypes.c_int), ("keep_samples", ctypes.c_int),
-                ("max_launch_rows", ctypes.c_int)]
+                ("max_launch_rows", ctypes.c_int), ("min_launch_rows", ctypes.c_int),
+                ("max_launch_wait_us", ctypes.c_int)]
 
 
 class GzRunnerStats(ctypes.Structure):

@@ -41,6 +41,7 @@ struct Pool {
     float* h_val = nullptr;
     int rows = 0;                    // rows submitted in the current launch
     int rows_done = 0;               // rows whose predictions are in h_out (engine side)
+    std::chrono::steady_clock::time_point queued_at;   // set under qm when queued
     std::atomic<int> state{kEngine};
 };
 
@@ -140,6 +141,7 @@ static void engine_main(gz_runner* r, int tid) {
             p.state.store(kQueued, std::memory_order_release);
             {
                 std::lock_guard<std::mutex> lk(r->qm);
+                r->pools[i].queued_at = std::chrono::steady_clock::now();
                 r->queue.push_back(i);
             }
             r->qcv.notify_one();
@@ -171,6 +173,12 @@ static void launcher_main(gz_runner* r) {
         return;
     }
     const int max_rows = r->cfg.max_launch_rows > 0 ? r->cfg.max_launch_rows : 1 << 30;
+    // Launch batching: while the GPU still has a batch in flight, hold the next launch until
+    // min_launch_rows rows are queued or its oldest pool has waited max_launch_wait_us.  The engine
+    // threads keep working on their other pools meanwhile, and a larger launch runs the two-boards
+    // per workgroup kernel, which needs half the L2 weight stream per board.
+    const int min_rows = r->cfg.min_launch_rows;
+    const auto max_wait = std::chrono::microseconds(r->cfg.max_launch_wait_us > 0 ? r->cfg.max_launch_wait_us : 0);
     std::deque<int> inflight;        // indices into batches_ring, oldest first
     int next_slot = 0;
     std::vector<gz_segment> segs;
@@ -227,6 +235,18 @@ static void launcher_main(gz_runner* r) {
                     r->qcv.wait_for(lk, std::chrono::microseconds(200));
                 else
                     r->qcv.wait_for(lk, std::chrono::microseconds(30));
+            }
+            if (min_rows > 0 && !inflight.empty() && !r->queue.empty()) {
+                int queued = 0;
+                for (int i : r->queue) queued += r->pools[i].rows;
+                const auto deadline = r->pools[r->queue.front()].queued_at + max_wait;
+                if (queued < min_rows && (int)r->queue.size() < GZ_MAX_SEGMENTS &&
+                    std::chrono::steady_clock::now() < deadline) {
+                    // wait for more pools, the deadline, or (next loop) the batch in flight
+                    r->qcv.wait_until(lk, std::min(deadline, std::chrono::steady_clock::now() +
+                                                                 std::chrono::microseconds(100)));
+                    continue;
+                }
             }
             while (!r->queue.empty() && (int)b.pools.size() < GZ_MAX_SEGMENTS) {
                 const int i = r->queue.front();

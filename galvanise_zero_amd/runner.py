@@ -10,14 +10,15 @@ from . import _native, cppinterface
 class SelfPlayRunner(object):
     def __init__(self, hip_net, sm, transformer, conf, device=0, num_threads=8, pools_per_thread=2,
                  batch_size=256, seed=0, game_index_base=0, keep_samples=False, max_launch_rows=0,
-                 spin_yield_playouts=0):
+                 spin_yield_playouts=0, min_launch_rows=0, max_launch_wait_us=0):
         self.lib = _native.runner_lib()
         _native.engine_lib()
         self.net = hip_net
         self.sm = sm
         self.c_transformer = cppinterface.create_c_transformer(transformer)
         self.cfg = _native.GzRunnerConfig(device, num_threads, pools_per_thread, batch_size, seed,
-                                          game_index_base, 1, int(keep_samples), max_launch_rows)
+                                          game_index_base, 1, int(keep_samples), max_launch_rows,
+                                          min_launch_rows, max_launch_wait_us)
         self.conf = _native.make_selfplay_config(conf)
         # build extension (engine/config.h): 0 keeps the reference's never-yielding playout loop
         self.conf.puct_config.spin_yield_playouts = spin_yield_playouts

@@ -122,6 +122,8 @@ typedef struct gz_runner_config {
     int per_pool_unique_states;  /* pools always own their duplicate filter here (deterministic) */
     int keep_samples;            /* 1: queue samples for gz_runner_fetch_samples; 0: count and drop */
     int max_launch_rows;         /* cap on rows merged into one launch (0: no cap beyond 32 pools) */
+    int min_launch_rows;         /* hold a launch until this many rows are queued ... (0: launch at once) */
+    int max_launch_wait_us;      /* ... or its oldest pool has waited this long */
 } gz_runner_config;
 
 typedef struct gz_runner_stats {
