@@ -50,7 +50,10 @@ class GzNetDesc(ctypes.Structure):
                 ("value_hidden_size", ctypes.c_int),
                 ("num_values", ctypes.c_int),
                 ("leaky_relu", ctypes.c_int),
-                ("flatten_nchw", ctypes.c_int)]
+                ("flatten_nchw", ctypes.c_int),
+                ("conv_bias", ctypes.c_int),
+                ("value_bn", ctypes.c_int),
+                ("value_sigmoid", ctypes.c_int)]
 
 
 _FP = ctypes.POINTER(ctypes.c_float)
@@ -95,6 +98,9 @@ def make_net_desc(desc):
     d.value_hidden_size = desc.value_hidden_size
     d.num_values = desc.num_values
     d.leaky_relu = int(desc.leaky_relu)
+    d.conv_bias = int(getattr(desc, "conv_bias", False))
+    d.value_bn = int(getattr(desc, "value_bn", False))
+    d.value_sigmoid = int(getattr(desc, "value_sigmoid", False))
     d.flatten_nchw = int(desc.flatten_nchw)
     return d
 

@@ -76,6 +76,7 @@ struct KParams {
     Segment seg[kMaxSegments];
     unsigned long long* stamps;   // diagnostics only (GZ_KERNEL_STAMPS): [grid][8] s_memtime per phase
     int C, K0, B, R, VH, V, leaky, flatten_nchw, maxP, npos;
+    int value_sigmoid;       // legacy model files: independent sigmoid per value output
     int btab_off;            // LDS byte offset of the trunk bias table
     int P[kMaxRoles];
 };
@@ -676,14 +677,18 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
                 o[v] = wave_sum(s) + kp.vdb[v];
             }
             if (lane == 0) {
-                float m = o[0];
-                for (int v = 1; v < kp.V; ++v) m = fmaxf(m, o[v]);
-                float e[4], sum = 0.f;
-                for (int v = 0; v < kp.V; ++v) { e[v] = __expf(o[v] - m); sum += e[v]; }
                 const int board = board0 + b;
                 const int sg = find_segment(kp, board);
                 float* out = kp.seg[sg].val + (size_t)(board - kp.seg[sg].row0) * kp.V;
-                for (int v = 0; v < kp.V; ++v) out[v] = e[v] / sum;
+                if (kp.value_sigmoid) {
+                    for (int v = 0; v < kp.V; ++v) out[v] = 1.f / (1.f + __expf(-o[v]));
+                } else {
+                    float m = o[0];
+                    for (int v = 1; v < kp.V; ++v) m = fmaxf(m, o[v]);
+                    float e[4], sum = 0.f;
+                    for (int v = 0; v < kp.V; ++v) { e[v] = __expf(o[v] - m); sum += e[v]; }
+                    for (int v = 0; v < kp.V; ++v) out[v] = e[v] / sum;
+                }
             }
         }
     }

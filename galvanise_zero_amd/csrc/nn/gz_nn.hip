@@ -140,6 +140,8 @@ static size_t spec_count(const gz_net_desc& d) {
     n += (size_t)d.residual_layers * 2 * (k * k * F * F + 4 * F);
     for (int r = 0; r < d.role_count; ++r) n += F * 2 + 4 * 2 + 2 * HW * d.policy_dist_count[r] + d.policy_dist_count[r];
     n += F + HW * d.value_hidden_size + d.value_hidden_size + (size_t)d.value_hidden_size * d.num_values + d.num_values;
+    if (d.conv_bias) n += F + (size_t)d.residual_layers * 2 * F + (size_t)d.role_count * 2 + 1;
+    if (d.value_bn) n += 4;
     return n;
 }
 
@@ -199,6 +201,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     kp.V = d.num_values;
     kp.leaky = d.leaky_relu;
     kp.flatten_nchw = d.flatten_nchw;
+    kp.value_sigmoid = d.value_sigmoid;
     kp.maxP = maxP;
     kp.npos = npos;
     for (int r = 0; r < d.role_count; ++r) kp.P[r] = d.policy_dist_count[r];
@@ -288,7 +291,9 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     std::vector<float> wh((size_t)HC * F), bh(HC, 0.f);
 
     Cursor cur{blob};
-    auto bn_fold = [&](int n, std::vector<float>& scale, std::vector<float>& bias) {
+    // BN after a conv with bias cb (legacy model files): gamma*(conv + cb - mean)/sqrt(var+eps) + beta
+    // = scale*conv + (beta + (cb - mean)*scale)
+    auto bn_fold = [&](int n, std::vector<float>& scale, std::vector<float>& bias, const float* cb = nullptr) {
         const float* g = cur.take(n);
         const float* be = cur.take(n);
         const float* mu = cur.take(n);
@@ -297,13 +302,15 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
         bias.resize(n);
         for (int i = 0; i < n; ++i) {
             scale[i] = g[i] / std::sqrt(var[i] + eps);
-            bias[i] = be[i] - mu[i] * scale[i];
+            bias[i] = cb ? be[i] + (cb[i] - mu[i]) * scale[i] : be[i] - mu[i] * scale[i];
         }
     };
+    auto conv_bias = [&](int n) -> const float* { return d.conv_bias ? cur.take(n) : nullptr; };
     std::vector<float> s, bb;
     {   // initial conv [3][3][C][F] -> w0[kc][co][32], k = tap*C + c
         const float* w = cur.take((size_t)9 * C * F);
-        bn_fold(F, s, bb);
+        const float* cb = conv_bias(F);
+        bn_fold(F, s, bb, cb);
         for (int co = 0; co < F; ++co) {
             b0[co] = bb[co];
             for (int k = 0; k < 9 * C; ++k) {
@@ -315,7 +322,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     }
     for (int conv = 0; conv < 2 * B; ++conv) {  // [3][3][F][F] -> [tap][kc][co][32]
         const float* w = cur.take((size_t)9 * F * F);
-        bn_fold(F, s, bb);
+        const float* cb = conv_bias(F);
+        bn_fold(F, s, bb, cb);
         uint16_t* dst = wres.data() + (size_t)conv * 9 * F * F;
         for (int co = 0; co < F; ++co) {
             bres[(size_t)conv * F + co] = bb[co];
@@ -329,7 +337,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     std::vector<const float*> pdense(R), pbias(R);
     for (int r = 0; r < R; ++r) {
         const float* w = cur.take((size_t)F * 2);   // [1][1][F][2]
-        bn_fold(2, s, bb);
+        const float* cb = conv_bias(2);
+        bn_fold(2, s, bb, cb);
         for (int c = 0; c < 2; ++c) {
             for (int f = 0; f < F; ++f) wh[(size_t)(2 * r + c) * F + f] = w[(size_t)f * 2 + c] * s[c];
             bh[2 * r + c] = bb[c];
@@ -339,8 +348,15 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     }
     {
         const float* w = cur.take(F);   // [1][1][F][1], no BN, no bias (model.py:275-279)
-        for (int f = 0; f < F; ++f) wh[(size_t)(2 * R) * F + f] = w[f];
-        bh[2 * R] = 0.f;
+        const float* cb = conv_bias(1);  // legacy files: bias, then BN (value_bn)
+        float vs = 1.f, vb = cb ? cb[0] : 0.f;
+        if (d.value_bn) {
+            bn_fold(1, s, bb, cb);
+            vs = s[0];
+            vb = bb[0];
+        }
+        for (int f = 0; f < F; ++f) wh[(size_t)(2 * R) * F + f] = w[f] * vs;
+        bh[2 * R] = vb;
     }
     const float* vhw = cur.take((size_t)HW * d.value_hidden_size);
     const float* vhb = cur.take(d.value_hidden_size);

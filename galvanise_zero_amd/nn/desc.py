@@ -42,6 +42,13 @@ class NetDesc:
     # Keras >= 2.1.6 Flatten under channels_first permutes to (H, W, C) before flattening; the
     # legacy (keras 2.1.3) model files flatten in (C, H, W) order.  See SURVEY appendix A.
     flatten_nchw: bool = False
+    # Legacy v1 model files (keras 2.1.3-2.1.5, e.g. data/breakthrough/models/x6_102.json): every
+    # Conv2D carries a bias, the value head's 1x1 conv is followed by BatchNormalization, and the
+    # value Dense uses sigmoid.  Off for the current model.py (use_bias=False, model.py:25-44,
+    # value conv do_bn=False :275-279, softmax :287-291).
+    conv_bias: bool = False
+    value_bn: bool = False
+    value_sigmoid: bool = False
 
     @property
     def role_count(self):
@@ -82,19 +89,26 @@ def weight_spec(d: NetDesc) -> List[Tuple[str, Tuple[int, ...]]]:
         spec.extend([(prefix + "_gamma", (n,)), (prefix + "_beta", (n,)),
                      (prefix + "_mean", (n,)), (prefix + "_var", (n,))])
 
-    spec.append(("initial_conv", (k, k, C, F)))
+    def conv(name, shape):
+        spec.append((name, shape))
+        if d.conv_bias:                     # Keras Conv2D weights: [kernel, bias]
+            spec.append((name + "_bias", (shape[3],)))
+
+    conv("initial_conv", (k, k, C, F))
     bn("initial_bn", F)
     for i in range(d.residual_layers):
-        spec.append(("res%d_conv0" % i, (k, k, F, F)))
+        conv("res%d_conv0" % i, (k, k, F, F))
         bn("res%d_bn0" % i, F)
-        spec.append(("res%d_conv1" % i, (k, k, F, F)))
+        conv("res%d_conv1" % i, (k, k, F, F))
         bn("res%d_bn1" % i, F)
     for r, p in enumerate(d.policy_dist_count):
-        spec.append(("policy%d_conv" % r, (1, 1, F, 2)))
+        conv("policy%d_conv" % r, (1, 1, F, 2))
         bn("policy%d_bn" % r, 2)
         spec.append(("policy%d_dense" % r, (2 * d.hw, p)))
         spec.append(("policy%d_bias" % r, (p,)))
-    spec.append(("value_conv", (1, 1, F, 1)))
+    conv("value_conv", (1, 1, F, 1))
+    if d.value_bn:
+        bn("value_bn", 1)
     spec.append(("value_hidden", (d.hw, d.value_hidden_size)))
     spec.append(("value_hidden_bias", (d.value_hidden_size,)))
     spec.append(("value_dense", (d.value_hidden_size, d.num_values)))

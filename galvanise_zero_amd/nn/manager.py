@@ -45,6 +45,19 @@ class Manager(object):
         transformer = self.get_transformer(game, generation_descr)
         return NeuralNetwork(transformer, HipModel(desc, weights, self.device), generation_descr)
 
+    def network_from_keras(self, game, model_json, layer_weights, generation_descr=None):
+        """A reference model file (data/<game>/models/<gen>.json) + its per-layer weights (dict or an
+        .npz of '<layer>/<i>' arrays, see nn/keras_model.py) -> NeuralNetwork on the HIP forward.
+        Replaces load_network's Keras model_from_json + load_weights (manager.py:129-139)."""
+        from . import keras_model
+        if isinstance(layer_weights, str):
+            layer_weights = keras_model.load_layer_weights_npz(layer_weights)
+        desc, weights = keras_model.weights_from_keras(model_json, layer_weights)
+        if generation_descr is None:
+            generation_descr = templates.default_generation_desc(game, num_previous_states=1,
+                                                                 draw_head=desc.num_values == 3)
+        return self.network_from_desc(game, desc, weights, generation_descr)
+
     def _path(self, game, sub, name, ext):
         p = os.path.join(self.data_path, game, sub)
         os.makedirs(p, exist_ok=True)

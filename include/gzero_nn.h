@@ -35,6 +35,10 @@ typedef struct gz_net_desc {
     int num_values;                           /* 2, or 3 with a draw head           */
     int leaky_relu;                           /* 0: relu, 1: LeakyReLU(alpha=0.03)  */
     int flatten_nchw;                         /* 0: Keras>=2.1.6 (H,W,C) flatten; 1: legacy (C,H,W) */
+    /* legacy v1 model files (data/breakthrough/models/x6_102.json, keras 2.1.3): */
+    int conv_bias;                            /* every Conv2D has use_bias: a bias after each kernel */
+    int value_bn;                             /* BatchNormalization after the value head's 1x1 conv  */
+    int value_sigmoid;                        /* value Dense activation sigmoid (else softmax)      */
 } gz_net_desc;
 
 typedef struct gz_net gz_net;

@@ -14,6 +14,9 @@ executed by Keras 2.2 / TF 1.12 ``predict_on_batch`` (``src/ggpzero/util/cppinte
   Dense(V) softmax
 * Flatten: channels_first data in Keras >= 2.1.6 is permuted to (H, W, C) before flattening
   (``flatten_nchw=False``); legacy files flatten (C, H, W).
+* Legacy v1 model files (data/breakthrough/models/x6_102.json, keras 2.1.3): Conv2D(use_bias=True)
+  everywhere (``conv_bias``), BatchNormalization after the value head's conv (``value_bn``), value
+  Dense with sigmoid (``value_sigmoid``).
 
 Arithmetic is float64 (the fp32 TF result is within ~1e-6 of it); outputs are float32 like
 ``predict_on_batch``.  Parity of the reference NN itself is *unpinned*: no reference test holds a
@@ -63,30 +66,48 @@ def _flatten(x, nchw):
     return x.reshape(x.shape[0], -1)
 
 
+def _sigmoid(z):
+    return 1.0 / (1.0 + np.exp(-z))
+
+
+def _value_out(desc, z):
+    return (_sigmoid(z) if getattr(desc, "value_sigmoid", False) else _softmax(z)).astype(np.float32)
+
+
 def forward(desc, weights, planes):
     """planes: float32 [N, C, H, W] (the poll() layout, cppinterface.py:114).
 
     Returns [policy_0 [N,P_0], ..., policy_{R-1}, value [N,V]] float32 (model.py:294 order)."""
     w = dict(weights)
     leaky = desc.leaky_relu
+
+    def conv(x, name):
+        y = _conv_same(x, w[name])
+        if getattr(desc, "conv_bias", False):
+            y = y + w[name + "_bias"].astype(np.float64)
+        return y
+
     x = np.transpose(planes.astype(np.float64), (0, 2, 3, 1))     # NHWC
-    x = _act(_bn(_conv_same(x, w["initial_conv"]), w, "initial_bn"), leaky)
+    x = _act(_bn(conv(x, "initial_conv"), w, "initial_bn"), leaky)
     for i in range(desc.residual_layers):
         t = x
-        y = _act(_bn(_conv_same(x, w["res%d_conv0" % i]), w, "res%d_bn0" % i), leaky)
-        y = _bn(_conv_same(y, w["res%d_conv1" % i]), w, "res%d_bn1" % i)
+        y = _act(_bn(conv(x, "res%d_conv0" % i), w, "res%d_bn0" % i), leaky)
+        y = _bn(conv(y, "res%d_conv1" % i), w, "res%d_bn1" % i)
         x = _act(t + y, leaky)
     outs = []
     for r in range(desc.role_count):
-        h = _act(_bn(_conv_same(x, w["policy%d_conv" % r]), w, "policy%d_bn" % r), leaky)
+        h = _act(_bn(conv(x, "policy%d_conv" % r), w, "policy%d_bn" % r), leaky)
         logits = _flatten(h, desc.flatten_nchw) @ w["policy%d_dense" % r].astype(np.float64)
         logits = logits + w["policy%d_bias" % r]
         outs.append(_softmax(logits).astype(np.float32))
-    v = _act(_conv_same(x, w["value_conv"]), leaky)
+    v = conv(x, "value_conv")
+    if getattr(desc, "value_bn", False):
+        v = _bn(v, w, "value_bn")
+    v = _act(v, leaky)
     hid = _act(_flatten(v, desc.flatten_nchw) @ w["value_hidden"].astype(np.float64)
                + w["value_hidden_bias"], leaky)
     val = hid @ w["value_dense"].astype(np.float64) + w["value_bias"]
-    outs.append(_softmax(val).astype(np.float32))
+    outs.append(_value_out(desc, val))
     return outs
 
 
@@ -107,6 +128,8 @@ def _fold(w, conv, bn):
     k = w[conv].astype(np.float32)
     g, b, m, v = (w[bn + s].astype(np.float32) for s in ("_gamma", "_beta", "_mean", "_var"))
     s = g / np.sqrt(v + np.float32(EPS))
+    if conv + "_bias" in w:                 # legacy conv bias folds into the BN shift
+        return (k * s).astype(np.float32), (b + (w[conv + "_bias"].astype(np.float32) - m) * s).astype(np.float32)
     return (k * s).astype(np.float32), (b - m * s).astype(np.float32)
 
 
@@ -129,9 +152,16 @@ def forward_bf16_emulated(desc, weights, planes):
         h = _act(_conv_same(x, k) + b, leaky)
         logits = _flatten(h, desc.flatten_nchw) @ w["policy%d_dense" % r].astype(np.float64)
         outs.append(_softmax(logits + w["policy%d_bias" % r]).astype(np.float32))
-    v = _act(_conv_same(x, w["value_conv"]), leaky)
+    if getattr(desc, "value_bn", False):
+        k, b = _fold(w, "value_conv", "value_bn")
+        v = _act(_conv_same(x, k) + b, leaky)
+    else:
+        v = _conv_same(x, w["value_conv"])
+        if "value_conv_bias" in w:
+            v = v + w["value_conv_bias"]
+        v = _act(v, leaky)
     hid = _act(_flatten(v, desc.flatten_nchw) @ w["value_hidden"].astype(np.float64)
                + w["value_hidden_bias"], leaky)
     val = hid @ w["value_dense"].astype(np.float64) + w["value_bias"]
-    outs.append(_softmax(val).astype(np.float32))
+    outs.append(_value_out(desc, val))
     return outs

@@ -26,17 +26,19 @@ def torch_forward(desc, weights, planes):
     act = (lambda t: tF.leaky_relu(t, 0.03)) if desc.leaky_relu else tF.relu
     x = torch.tensor(planes, dtype=torch.float64)
 
-    def conv(t, k):
-        return tF.conv2d(t, k.permute(3, 2, 0, 1), padding=k.shape[0] // 2)
+    def conv(t, name):
+        k = w[name] if isinstance(name, str) else name
+        b = w.get(name + "_bias") if isinstance(name, str) and desc.conv_bias else None
+        return tF.conv2d(t, k.permute(3, 2, 0, 1), bias=b, padding=k.shape[0] // 2)
 
     def bn(t, p):
         return tF.batch_norm(t, w[p + "_mean"], w[p + "_var"], w[p + "_gamma"], w[p + "_beta"],
                              training=False, eps=1e-3)
 
-    x = act(bn(conv(x, w["initial_conv"]), "initial_bn"))
+    x = act(bn(conv(x, "initial_conv"), "initial_bn"))
     for i in range(desc.residual_layers):
-        y = act(bn(conv(x, w["res%d_conv0" % i]), "res%d_bn0" % i))
-        y = bn(conv(y, w["res%d_conv1" % i]), "res%d_bn1" % i)
+        y = act(bn(conv(x, "res%d_conv0" % i), "res%d_bn0" % i))
+        y = bn(conv(y, "res%d_conv1" % i), "res%d_bn1" % i)
         x = act(x + y)
 
     def flat(t):
@@ -46,12 +48,16 @@ def torch_forward(desc, weights, planes):
 
     outs = []
     for r in range(desc.role_count):
-        h = act(bn(conv(x, w["policy%d_conv" % r]), "policy%d_bn" % r))
+        h = act(bn(conv(x, "policy%d_conv" % r), "policy%d_bn" % r))
         z = flat(h) @ w["policy%d_dense" % r] + w["policy%d_bias" % r]
         outs.append(torch.softmax(z, 1).numpy())
-    v = act(conv(x, w["value_conv"]))
+    v = conv(x, "value_conv")
+    if desc.value_bn:
+        v = bn(v, "value_bn")
+    v = act(v)
     hid = act(flat(v) @ w["value_hidden"] + w["value_hidden_bias"])
-    outs.append(torch.softmax(hid @ w["value_dense"] + w["value_bias"], 1).numpy())
+    z = hid @ w["value_dense"] + w["value_bias"]
+    outs.append((torch.sigmoid(z) if desc.value_sigmoid else torch.softmax(z, 1)).numpy())
     return outs
 
 
@@ -60,6 +66,8 @@ VARIANTS = [
     NetDesc(5, 8, 8, 128, 2, [155, 155]),
     NetDesc(5, 8, 8, 64, 1, [65, 65], num_values=3, leaky_relu=True),
     NetDesc(5, 6, 6, 64, 1, [81, 81], flatten_nchw=True),
+    # legacy v1 model file semantics (x6_102.json): conv biases, value BN, sigmoid value
+    NetDesc(5, 8, 8, 64, 2, [155, 155], flatten_nchw=True, conv_bias=True, value_bn=True, value_sigmoid=True),
 ]
 
 
@@ -72,7 +80,7 @@ def test_oracle_matches_torch(desc):
     assert len(a) == desc.role_count + 1
     for u, v in zip(a, b):
         np.testing.assert_allclose(u, v, rtol=1e-5, atol=1e-6)
-    for u in a:
+    for u in (a[:-1] if desc.value_sigmoid else a):   # sigmoid value outputs are independent
         np.testing.assert_allclose(u.sum(axis=1), 1.0, atol=1e-5)
 
 
