@@ -1,0 +1,15 @@
+#!/bin/bash
+# PMC passes only (FETCH_SIZE | WRITE_SIZE | SQ counters), each its own rocprofv3 run, on the forward
+# at the launch sizes the batched bench runs (256 and 640 rows).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/pmc_r01k
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+KV="$R/tools/kernel_variants.py --configs 2 --batches 256,640 --reps 30 --variants default"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 $KV > $OUT/fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 $KV > $OUT/write.log 2>&1 || { echo "write pass failed"; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+    SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $OUT/sq -o sq -- \
+    python3 $KV > $OUT/sq.log 2>&1 || { echo "sq pass failed"; exit 1; }
+echo PMC OK

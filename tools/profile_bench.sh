@@ -10,7 +10,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-KV="$R/tools/kernel_variants.py --configs 2 --batches 256,512 --reps 30 --variants default"
+KV="$R/tools/kernel_variants.py --configs 2 --batches ${KV_BATCHES:-256,512} --reps 30 --variants default"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 $KV \
     > $OUT/fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 $KV \
