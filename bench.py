@@ -37,12 +37,12 @@ PEAK_BF16_TFLOPS = 2500.0      # gfx950 dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_L2_GBPS_PER_CU = 70.0
 NUM_CUS = 256
 # PMC-measured fabric bytes per trunk launch (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE,
-# separate rocprofv3 --pmc passes of tools/profile_bench.sh at 256 / 512 rows, profiles/r01d_pmc.txt).
+# separate rocprofv3 --pmc passes of tools/gpu_pmc.sh at 256 / 640 rows, profiles/r01k_pmc.txt).
 # PMC counters cannot be read inside the timed run, so the measured per-launch figure of the same
 # kernel at the bench's launch size is reported.
 TRAFFIC_PER_LAUNCH = {"gznn::trunk_kernel<128, 8, 8, 1, 1>": (14290.1 * 2 + 320.0) * 1024,
-                      "gznn::trunk_kernel<128, 8, 8, 2, 1>": (14581.6 * 2 + 640.0) * 1024}
-TRAFFIC_SOURCE = "profiles/r01d_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 256- and 512-row launches)"
+                      "gznn::trunk_kernel<128, 8, 8, 2, 1>": (14722.3 * 2 + 800.0) * 1024}
+TRAFFIC_SOURCE = "profiles/r01k_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 256- and 640-row launches)"
 
 
 def parse():
