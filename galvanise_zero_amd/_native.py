@@ -9,7 +9,7 @@ import os
 
 import numpy as np
 
-LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_DIR = os.environ.get("GZ_LIB_DIR") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")   # GZ_LIB_DIR: A/B builds (tools/)
 GZ_MAX_ROLES = 4
 
 _libs = {}

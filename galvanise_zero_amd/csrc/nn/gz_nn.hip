@@ -109,7 +109,10 @@ static KernelChoice variants(int v) {
 // there two boards per workgroup (21) win, each weight fragment feeding twice the MFMAs.  Every
 // variant computes each row identically (tests/test_nn_gpu.py::test_kernel_variants_identical), so
 // choosing per launch keeps results batch-invariant.
-constexpr int kSmallVariant = 11, kLargeVariant = 21, kLargeMinRows = 384;
+// Launches of 257-383 rows also take the two-board kernel: at one board per workgroup they would
+// need a second wave of workgroups on the 256 CUs (one trunk workgroup per CU by LDS).
+constexpr int kSmallVariant = 11, kLargeVariant = 21, kLargeMinRows = 257;
+constexpr int kCUs = 256;
 
 static KernelChoice select_kernel(int F, int H, int W, int v) {
 #define GZ_CASE(F_, H_, W_) \
@@ -573,3 +576,8 @@ extern "C" int gz_net_stamp_avg(const gz_net* net, double* out8) {
 extern "C" float gz_net_last_kernel_ms(const gz_net* net) { return net ? net->last_ms : 0.f; }
 
 extern "C" int gz_net_large_min_rows(const gz_net* net) { return net ? net->large_min_rows : 0; }
+
+extern "C" int gz_net_wave_rows(const gz_net* net) {
+    if (!net) return 0;
+    return (net->large_min_rows < (1 << 30) ? net->large.nb : net->small.nb) * kCUs;
+}

@@ -93,6 +93,10 @@ float gz_net_last_kernel_ms(const gz_net* net);
  * the one-board variant (both compute every row identically). */
 int gz_net_large_min_rows(const gz_net* net);
 
+/* Rows one full wave of workgroups of the large variant covers (boards per workgroup x 256 CUs,
+ * one trunk workgroup per CU): the native runner launches multiples of it beyond one wave. */
+int gz_net_wave_rows(const gz_net* net);
+
 /* Algorithmic FLOPs of one leaf evaluation (2 FLOP/MAC). */
 double gz_net_flops_per_eval(const gz_net* net);
 
