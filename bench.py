@@ -212,10 +212,11 @@ def main():
     totals, T = shard.reduce_counters(
         [d["rows"], d["batches"], d["games_completed"], d["games_with_samples"], d["samples"], d["kernel_ms"],
          d["kernel_launches"], d["segments"], s1["games_completed"], s1["completed_game_evals"], d["trunk_ms"],
-         d["large_launches"], d["large_rows"], d["large_trunk_ms"], d["engine_idle_ms"]],
+         d["large_launches"], d["large_rows"], d["large_trunk_ms"], d["engine_idle_ms"],
+         d["no_samples"], d["resigns"], d["aborts"], d["dupes"]],
         elapsed, device="cuda")
     (rows, batches, games, games_s, samples, kms, launches, segments, games_all, game_evals_all, tms,
-     l_launches, l_rows, l_tms, idle_ms) = totals
+     l_launches, l_rows, l_tms, idle_ms, no_samples, resigns, aborts, dupes) = totals
 
     if rank == 0:
         flops = desc.flops_per_eval()
@@ -255,6 +256,9 @@ def main():
             "games_completed_total": games_all,
             "sample_games_per_sec": games_s / T,
             "samples_per_sec": samples / T,
+            # selfplaymanager.cpp:161-200 counters over the window
+            "selfplay_counters": {"no_sample_games": no_samples, "resigns": resigns, "aborts": aborts,
+                                  "duplicate_states": dupes},
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,

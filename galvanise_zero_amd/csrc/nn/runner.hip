@@ -173,10 +173,11 @@ static void launcher_main(gz_runner* r) {
         return;
     }
     const int max_rows = r->cfg.max_launch_rows > 0 ? r->cfg.max_launch_rows : 1 << 30;
-    // Launch batching: while the GPU still has a batch in flight, hold the next launch until
-    // min_launch_rows rows are queued or its oldest pool has waited max_launch_wait_us.  The engine
-    // threads keep working on their other pools meanwhile, and a larger launch runs the two-boards
-    // per workgroup kernel, which needs half the L2 weight stream per board.
+    // Launch batching: hold a launch until min_launch_rows rows are queued or its oldest pool has
+    // waited max_launch_wait_us - also when the GPU is idle, which in the host-bound regime is most
+    // of the time (otherwise single-pool launches dominate).  The engine threads keep working on
+    // their other pools meanwhile, and a larger launch runs the two-boards-per-workgroup kernel,
+    // which needs half the L2 weight stream per board.
     const int min_rows = r->cfg.min_launch_rows;
     const int wave_rows = gz_net_wave_rows(r->net);   // rows of one full wave of the large kernel
     const auto max_wait = std::chrono::microseconds(r->cfg.max_launch_wait_us > 0 ? r->cfg.max_launch_wait_us : 0);
@@ -237,7 +238,7 @@ static void launcher_main(gz_runner* r) {
                 else
                     r->qcv.wait_for(lk, std::chrono::microseconds(30));
             }
-            if (min_rows > 0 && !inflight.empty() && !r->queue.empty()) {
+            if (min_rows > 0 && !r->queue.empty()) {
                 int queued = 0;
                 for (int i : r->queue) queued += r->pools[i].rows;
                 const auto deadline = r->pools[r->queue.front()].queued_at + max_wait;
