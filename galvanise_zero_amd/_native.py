@@ -57,6 +57,15 @@ class GzNetDesc(ctypes.Structure):
 
 
 _FP = ctypes.POINTER(ctypes.c_float)
+GZ_MAX_SEGMENTS = 32
+
+
+class GzSegment(ctypes.Structure):
+    """gz_segment (include/gzero_nn.h): one run of boards of a segmented launch."""
+    _fields_ = [("rows", ctypes.c_int),
+                ("planes", ctypes.c_void_p),
+                ("policies", ctypes.c_void_p * GZ_MAX_ROLES),
+                ("values", ctypes.c_void_p)]
 
 
 def nn_lib():
@@ -74,6 +83,8 @@ def nn_lib():
         lib.gz_net_forward_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                               ctypes.c_void_p]
+        lib.gz_net_forward_segments.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(GzSegment),
+                                                ctypes.c_int]
         lib.gz_net_last_kernel_ms.restype = ctypes.c_float
         lib.gz_net_last_kernel_ms.argtypes = [ctypes.c_void_p]
         lib.gz_net_stamp_avg.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
@@ -154,6 +165,21 @@ class HipNet(object):
                                                    ctypes.c_void_p(d_values)),
                     "gz_net_forward_device")
 
+    def forward_segments(self, stream, segments):
+        """Asynchronous segmented launch on `stream`: segments = [(rows, planes_ptr, [policy_ptr per
+        role], values_ptr)]; pointers are device or pinned host addresses."""
+        if not 1 <= len(segments) <= GZ_MAX_SEGMENTS:
+            raise ValueError("1..%d segments" % GZ_MAX_SEGMENTS)
+        segs = (GzSegment * len(segments))()
+        for s, (rows, planes, pols, vals) in zip(segs, segments):
+            s.rows = rows
+            s.planes = planes
+            for r, p in enumerate(pols):
+                s.policies[r] = p
+            s.values = vals
+        self._check(self.lib.gz_net_forward_segments(self.handle, ctypes.c_void_p(stream), segs, len(segments)),
+                    "gz_net_forward_segments")
+
     def last_kernel_ms(self):
         return self.lib.gz_net_last_kernel_ms(self.handle)
 
@@ -230,7 +256,7 @@ class GzPoolStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_long) for n in (
         "games_started", "games_completed", "games_with_samples", "samples", "no_samples", "dupes",
         "resigns", "false_positive_resigns0", "false_positive_resigns1", "early_run_to_ends",
-        "aborts_game_length", "evaluations", "polls", "completed_game_evals")]
+        "aborts_game_length", "evaluations", "polls", "completed_game_evals", "tree_playouts")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -287,6 +313,8 @@ _ENGINE_SIGS = {
     "gz_player_root_children": (ctypes.c_int, [_VP, _IP, ctypes.POINTER(ctypes.c_uint32), _FP, ctypes.c_int]),
     "gz_unique_states_create": (_VP, [_VP, _VP, ctypes.c_int]),
     "gz_unique_states_destroy": (None, [_VP]),
+    "gz_unique_states_clear": (ctypes.c_int, [_VP]),
+    "gz_pool_clear_unique_states": (ctypes.c_int, [_VP]),
     "gz_pool_create": (_VP, [_VP, _VP, ctypes.c_int, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_long, _VP,
                              _FP, ctypes.POINTER(_FP), _FP]),
     "gz_pool_destroy": (None, [_VP]),
@@ -382,7 +410,7 @@ class GzRunnerStats(ctypes.Structure):
                 ("resigns", ctypes.c_long), ("aborts", ctypes.c_long), ("dupes", ctypes.c_long),
                 ("segments", ctypes.c_long), ("completed_game_evals", ctypes.c_long),
                 ("large_launches", ctypes.c_long), ("large_rows", ctypes.c_long), ("large_trunk_ms", ctypes.c_double),
-                ("engine_idle_ms", ctypes.c_double)]
+                ("engine_idle_ms", ctypes.c_double), ("tree_playouts", ctypes.c_long)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -403,5 +431,6 @@ def runner_lib():
         lib.gz_runner_stop.argtypes = [_VP]
         lib.gz_runner_destroy.argtypes = [_VP]
         lib.gz_runner_last_error.restype = ctypes.c_char_p
+        lib.gz_runner_clear_unique_states.argtypes = [_VP]
         lib._gz_runner_typed = True
     return lib

@@ -112,6 +112,7 @@ static void to_stats(const PoolStats& s, gz_pool_stats* o) {
     o->evaluations = s.evaluations;
     o->polls = s.polls;
     o->completed_game_evals = s.completed_game_evals;
+    o->tree_playouts = s.tree_playouts;
 }
 
 // ---- JSON of samples (sampleToDict, supervisor_impl.cpp:75-118) ---------------------------------
@@ -429,6 +430,11 @@ extern "C" void gz_unique_states_destroy(gz_unique_states* u) {
         delete u;
     }
 }
+extern "C" int gz_unique_states_clear(gz_unique_states* u) {
+    if (!u) return fail("null unique states");
+    u->impl->clear();
+    return 0;
+}
 extern "C" gz_pool* gz_pool_create(const gz_sm* sm, const gz_transformer* t, int batch_size, const char* identifier,
                                    uint64_t seed, long game_index_base, gz_unique_states* unique_states,
                                    float* planes_buf, float* const* policy_bufs, float* value_buf) {
@@ -467,8 +473,16 @@ extern "C" int gz_pool_poll(gz_pool* p, int pred_count) {
     const int ts = p->impl->getTransformer()->totalSize();
     return p->impl->getReadyEvent()->buf_count / ts;
 }
+// the pool's own duplicate filter (pools created without a shared one); supervisor_impl.cpp:138-144
+extern "C" int gz_pool_clear_unique_states(gz_pool* p) {
+    if (!p) return fail("null pool");
+    if (p->own_unique) p->own_unique->clear();
+    return 0;
+}
 extern "C" int gz_pool_get_stats(gz_pool* p, gz_pool_stats* out) {
-    to_stats(p->impl->getStats(), out);
+    PoolStats s = p->impl->getStats();
+    s.tree_playouts = p->impl->treePlayouts();
+    to_stats(s, out);
     return 0;
 }
 extern "C" char* gz_pool_fetch_samples(gz_pool* p) {

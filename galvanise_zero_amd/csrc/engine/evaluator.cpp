@@ -951,7 +951,257 @@ int PuctEvaluator::treePlayout(PuctNode* current, Path& path) {
     for (int ii = 0; ii < sm->roleCount(); ii++) scores[ii] = current->getCurrentScore(ii);
     backup(scores, path);
     stats.num_tree_playouts++;
+    total_tree_playouts++;
     return (int)path.size();
+}
+
+// ---- root spin fast path ------------------------------------------------------------------------
+// With two or more finalised winning children at the root, the reference's playout loop is never
+// "converged" (the two most visited children are wins with equal scores) and runs until enough NN
+// evaluations accumulate -- up to millions of playouts per move, nearly all of them root -> win ->
+// backup with no evaluation (playoutMain, evaluator.cpp:744-886).  While the other candidates
+// provably cannot be selected, such a playout only needs the winning children's scores: spinPlayout
+// runs one playout of that form with the reference's arithmetic and RNG consumption (the root-latch
+// draw per reaching child), and returns false whenever the proof does not hold, after which the
+// ordinary treePlayout runs.
+//
+// An epoch (spinBuild, one pass over the children) establishes, for root visits v in [v0, v_end):
+//   * no child is in flight, none is unselectable or being expanded, the Dirichlet noise cannot
+//     change, backup_finalised is off (the root cannot become finalised);
+//   * every non-win candidate i scores at most U_i = base_i + (float)(pc(v_end-1) * p_i) *
+//     sqrt(v_end) / (t_i + 1), the value its exploration term reaches at the epoch's last playout
+//     (pc and sqrt increase with v, its traversals and policy_prob do not change inside the epoch:
+//     it is never selected and normaliseX -- every 100 root visits -- ends the epoch), with base_i =
+//     its current score, or for unexpanded children the FPU prior, bounded by the top win's score;
+//   * the best win scores at least min_w s_w * (1 + pc(v0)) > max_i U_i (with a relative margin
+//     covering the float truncations of the selection's comparisons);
+//   * the two most visited children are wins with equal scores, so converged() is false for the
+//     whole epoch (only wins gain visits), and no non-win can reach the root latch threshold.
+// Per playout only the winning children are scored, in the order sortedChildrenSelect gives them
+// (constant inside the epoch: no sort key changes), with the reference loop's `score > best_score`
+// (float) semantics: exact ties between wins resolve as in the reference.
+
+static bool spin_fast_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("GZ_SPIN_FAST");
+        return !(e != nullptr && e[0] == '0');
+    }();
+    return v;
+}
+
+bool PuctEvaluator::spinBuild() {
+    spin.valid = false;
+    PuctNode* node = root;
+    if (conf->backup_finalised || conf->think_time > 0) return false;
+    if (node->is_finalised || node->isTerminal() || node->num_children < 2 || node->visits <= 8) return false;
+    if (node->inflight_visits != 0) return false;
+    const int lead = node->lead_role_index;
+    if (lead < 0) return false;
+    if (!node->dirichlet_noise_set && conf->dirichlet_noise_pct >= 0 && node->getCurrentScore(lead) <= 0.95)
+        return false;
+
+    const uint32_t v0 = node->visits;
+    PuctNodeChild* cs = node->children();
+    const int n = node->num_children;
+    int nw = 0, reach = 0;
+    float win_score = 0.f;
+    uint32_t wv0 = 0, wv1 = 0;   // the two largest win visit counts
+    uint32_t nonwin_max_visits = 0;
+    bool have_nonwin_visits = false;
+    for (int i = 0; i < n; ++i) {
+        const PuctNodeChild* c = cs + i;
+        const PuctNode* cn = c->to_node;
+        if (c->unselectable) return false;
+        if (cn != nullptr) {
+            if (cn->inflight_visits != 0) return false;
+            if (cn->num_children > 0 && cn->unselectable_count == cn->num_children) return false;
+            if (cn->is_finalised) {
+                const float sc = cn->getCurrentScore(lead);
+                if (sc > 0.99) {
+                    if (!cn->isTerminal() || nw == 8) return false;
+                    if (nw > 0 && !(sc == win_score)) return false;
+                    win_score = sc;
+                    spin.wins[nw++] = (uint16_t)i;
+                    if (cn->visits >= wv0) { wv1 = wv0; wv0 = cn->visits; }
+                    else if (cn->visits > wv1) wv1 = cn->visits;
+                    ++reach;
+                    continue;
+                }
+                if (sc < 0.01) continue;   // bad_fallback candidate: never reached while a candidate exists
+            }
+            have_nonwin_visits = true;
+            nonwin_max_visits = std::max(nonwin_max_visits, cn->visits);
+        }
+        // a non-win candidate: the latch threshold only gets further away as v grows (checked
+        // whether or not the latch is active yet: it may become active inside the epoch)
+        if (c->traversals > 16 && c->traversals > node->visits * 0.66f) return false;
+        ++reach;
+    }
+    if (nw < 2) return false;
+    // converged() (evaluator.cpp:1342-1362) compares the two most visited children: both wins with
+    // equal scores -> false, and it stays false while only wins gain visits; otherwise playoutMain
+    // evaluates it as usual
+    const bool conv_false = !(have_nonwin_visits && !(nonwin_max_visits < wv1));
+
+    // the FPU prior of unexpanded children: the top-visits child is a win (chooseTopVisits returns
+    // the first win), so prior = win score - fpu * sqrt(...) <= win score
+    const double prior_bound = (double)win_score;
+    const float cpuct_base_id = 19652.0f;
+    auto pc_at = [&](uint32_t v) {
+        float p = std::log((1 + v + cpuct_base_id) / cpuct_base_id);
+        p += conf->puct_constant_root;
+        return p;
+    };
+    // the best win scores at least its child_score = s_w * (1 + pc(v)) >= s_w * (1 + pc(v0))
+    double floor_win = win_score;
+    floor_win *= 1.0f + pc_at(v0);
+    const double floor_adj = floor_win - std::fabs(floor_win) * 1e-6 - 1e-12;
+
+    uint32_t v_end = (v0 / 100 + 1) * 100;   // normaliseX at the backup reaching a multiple of 100
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        const uint32_t vl = v_end - 1;         // the epoch's last selection
+        const float pc = pc_at(vl);
+        const double sq = std::sqrt(vl + 1);
+        double bound = -1e300;
+        for (int i = 0; i < n; ++i) {
+            const PuctNodeChild* c = cs + i;
+            const PuctNode* cn = c->to_node;
+            double base, expl;
+            if (cn == nullptr) {
+                base = prior_bound;
+                expl = pc * c->policy_prob * sq / (c->traversals + 1 + 0.0);
+            } else {
+                const float sc = cn->getCurrentScore(lead);
+                if (cn->is_finalised && (sc > 0.99 || sc < 0.01)) continue;   // wins / bad fallbacks
+                base = sc;
+                expl = cn->is_finalised ? 0.0 : pc * c->policy_prob * sq / (c->traversals + 1 + 0.0);
+            }
+            bound = std::max(bound, base + expl);
+        }
+        const double bound_adj = bound + std::fabs(bound) * 1e-6 + 1e-12;
+        if (bound_adj < floor_adj) {
+            // the wins in sortedChildrenSelect order (evaluator.cpp:242-263; equal-score wins are
+            // equivalent under its comparator, so std::sort's permutation decides)
+            SelectScratch& S = t_sel;
+            S.reserve(n);
+            for (int i = 0; i < n; ++i) {
+                const PuctNode* cn = cs[i].to_node;
+                S.key_s[i] = cn == nullptr ? -1 : cn->getCurrentScore(lead);
+                S.key_p[i] = cs[i].policy_prob_orig;
+            }
+            const uint16_t* order = S.sortedOrder(n);
+            int k = 0;
+            for (int j = 0; j < n; ++j) {
+                const PuctNode* cn = cs[order[j]].to_node;
+                if (cn != nullptr && cn->is_finalised && cn->getCurrentScore(lead) > 0.99) spin.wins[k++] = order[j];
+            }
+            if (k != nw) return false;
+            spin.conv_false = conv_false;
+            spin.root = node;
+            spin.v_end = v_end;
+            spin.reach = reach;
+            spin.nwins = nw;
+            spin.nonwin_bound = bound_adj;
+            spin.valid = true;
+            return true;
+        }
+        const uint32_t k = (v_end - v0) / 4;
+        if (k == 0) break;
+        v_end = v0 + k;
+    }
+    return false;
+}
+
+bool PuctEvaluator::spinPlayout() {
+    if (!spin_fast_enabled()) return false;
+    PuctNode* node = root;
+    if (!spin.valid || spin.root != node || node->visits >= spin.v_end) {
+        if (spin.root == node && node->visits < spin.retry_at) return false;
+        if (!spinBuild()) {
+            spin.root = node;
+            spin.retry_at = node->visits + 8;
+            return false;
+        }
+    }
+    const int lead = node->lead_role_index;
+    if (node->inflight_visits != 0 ||
+        (!node->dirichlet_noise_set && conf->dirichlet_noise_pct >= 0 && node->getCurrentScore(lead) <= 0.95)) {
+        spin.valid = false;
+        return false;
+    }
+
+    // selectChild (evaluator.cpp:341-517) restricted to the winning children
+    setPuctConstant(node, 0);
+    const double sqrt_node_visits = std::sqrt(node->visits + 1);
+    PuctNodeChild* cs = node->children();
+    float best_score = -1;
+    int best = -1;
+    double min_score = 1e300;
+    const bool latch = node->visits > 1000 && node->visits < 40000000;
+    const float limit_latch_root = 0.66;
+    for (int k = 0; k < spin.nwins; ++k) {
+        const int i = spin.wins[k];
+        PuctNodeChild* c = cs + i;
+        const PuctNode* cn = c->to_node;
+        if (latch && c->traversals > 16 && c->traversals > node->visits * limit_latch_root) {
+            spin.valid = false;
+            return false;
+        }
+        const int traversals = c->traversals + 1;
+        const double inflight_visits = cn->inflight_visits;
+        const double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
+                                         (traversals + inflight_visits);
+        double child_score = cn->getCurrentScore(lead);
+        child_score *= 1.0f + node->puct_constant;
+        const double score = child_score + exploration_score;
+        min_score = std::min(min_score, score);
+        if (score > best_score) {   // the reference loop (evaluator.cpp:487-490), float best_score
+            best = i;
+            best_score = score;
+        }
+    }
+    // every win outscores every other candidate (the epoch bound), so the loop over all children
+    // in sorted order ends on the same child as this loop over the wins
+    if (!(spin.nonwin_bound < min_score) || !(spin.nonwin_bound <= (double)(float)min_score)) {
+        spin.valid = false;
+        return false;
+    }
+    PuctNodeChild* chosen = cs + best;
+
+    if (verify_fastpath()) {
+        // the ordinary selection from the same RNG state must pick the same child
+        const Rng before = rng;
+        for (int j = 0; latch && j < spin.reach; ++j) (void)rng.get();
+        const Rng after = rng;
+        rng = before;
+        Path tmp;
+        PuctNodeChild* ref = selectChild(node, tmp);
+        if (ref != chosen || !(rng == after)) {
+            std::fprintf(stderr, "gz spin fast-path mismatch (visits %u)\n", node->visits);
+            std::abort();
+        }
+        if (spin.conv_false && converged(conf->converged_visits)) {
+            std::fprintf(stderr, "gz spin fast-path: converged() is true\n");
+            std::abort();
+        }
+    } else if (latch) {
+        for (int j = 0; j < spin.reach; ++j) (void)rng.get();   // the root latch's per-child draws
+    }
+
+    // treePlayout (evaluator.cpp:658-720): root -> chosen (finalised terminal) -> backup
+    PuctNode* leaf = chosen->to_node;
+    Path& path = spin_path;
+    path.clear();
+    path.emplace_back(node, chosen, chosen);
+    node->inflight_visits++;
+    path.emplace_back(leaf, nullptr, nullptr);
+    stats.playouts_finals++;
+    float scores[kMaxRoles];
+    for (int ii = 0; ii < sm->roleCount(); ii++) scores[ii] = leaf->getCurrentScore(ii);
+    backup(scores, path);
+    stats.num_tree_playouts++;
+    total_tree_playouts++;
+    return true;
 }
 
 // evaluator.cpp:722-742
@@ -985,7 +1235,9 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
         const bool need_converged = use_think_time || stats.num_tree_playouts > max_tree_playouts ||
                                     stats.num_evaluations > max_evaluations ||
                                     stats.num_evaluations > max_non_converged_evaluations;
-        const bool is_converged = need_converged ? converged(conf->converged_visits) : false;
+        // inside a spin epoch converged() may be provably false (spinBuild)
+        const bool spin_epoch = spin.valid && spin.conv_false && spin.root == root && root->visits < spin.v_end;
+        const bool is_converged = need_converged && !spin_epoch ? converged(conf->converged_visits) : false;
 
         if (end_time > 0 && get_time() > end_time) break;
         if (root->is_finalised && stats.num_tree_playouts > 100) break;
@@ -1004,8 +1256,12 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
             }
         }
 
-        path.clear();
-        const int depth = treePlayout(root, path);
+        int depth = 2;
+        if (!spinPlayout()) {
+            spin.valid = false;
+            path.clear();
+            depth = treePlayout(root, path);
+        }
         stats.playouts_max_depth = std::max(depth, stats.playouts_max_depth);
         stats.playouts_total_depth += depth;
 
@@ -1101,6 +1357,7 @@ const PuctNodeChild* PuctEvaluator::onNextMove(int max_evaluations, double end_t
     GZ_ASSERT(root != nullptr && initial_root != nullptr);
     stats.reset();
     do_playouts = true;
+    spin = SpinEpoch();   // the root changed (a freed root's address may be reused)
 
     if (conf->think_time > 10 && !root->dirichlet_noise_set && !root->is_finalised && root->visits > 10000) {
         if (number_of_nodes < 3000000) resetRootNode();

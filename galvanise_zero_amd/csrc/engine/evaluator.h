@@ -79,6 +79,7 @@ public:
     };
     const PlayoutStats& getStats() const { return stats; }
     long totalEvaluations() const { return total_evaluations; }
+    long totalTreePlayouts() const { return total_tree_playouts; }
 
 private:
     void removeNode(PuctNode*);
@@ -96,6 +97,24 @@ private:
     int treePlayout(PuctNode* current, Path& path);
     void playoutWorker(int worker_id);
     void playoutMain(int max_evaluations, double end_time);
+
+    // Root spin fast path (evaluator.cpp, "spin"): playouts that go root -> finalised winning
+    // child, run without the full selection pass while provably nothing else can be chosen.
+    struct SpinEpoch {
+        const PuctNode* root = nullptr;
+        uint32_t v_end = 0;          // the epoch holds while root->visits < v_end
+        uint32_t retry_at = 0;       // after a failed build: next attempt at this root visit count
+        int reach = 0;               // selection candidates (root-latch RNG draws per playout)
+        int nwins = 0;
+        uint16_t wins[8];            // root children that are finalised wins, in sortedChildrenSelect order
+        double nonwin_bound = 0;     // upper bound of every other candidate's score until v_end
+        bool conv_false = false;     // converged() proved false for the epoch
+        bool valid = false;
+    };
+    bool spinBuild();
+    bool spinPlayout();
+    SpinEpoch spin;
+    Path spin_path;
 
     struct MaskedKey {
         std::vector<uint64_t> w;
@@ -122,6 +141,7 @@ private:
     int number_of_nodes = 0;
     long node_allocated_memory = 0;
     long total_evaluations = 0;
+    long total_tree_playouts = 0;   // diagnostics: NN-free playouts = tree playouts - evaluations
     bool do_playouts = false;
     PlayoutStats stats;
     Rng rng;

@@ -109,6 +109,7 @@ struct PoolStats {
     long evaluations = 0;          // NN rows requested
     long polls = 0;
     long completed_game_evals = 0; // NN evaluations consumed by the games counted in games_completed
+    long tree_playouts = 0;        // tree playouts of every game of the pool (filled by treePlayouts())
 };
 
 class SelfPlayManager {
@@ -132,6 +133,11 @@ public:
     void incrResigns() { stats.resigns++; }
     void incrAbortsGameLength() { stats.aborts_game_length++; }
     PoolStats& getStats() { return stats; }
+    long treePlayouts() const {
+        long n = 0;
+        for (const PuctEvaluator* pe : evaluators) n += pe->totalTreePlayouts();
+        return n;
+    }
 
     void startSelfPlayers(const SelfPlayConfig* config);
     void poll();

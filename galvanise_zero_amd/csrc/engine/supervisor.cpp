@@ -162,6 +162,7 @@ PoolStats Supervisor::stats() {
         s.evaluations += p.evaluations;
         s.polls += p.polls;
         s.completed_game_evals += p.completed_game_evals;
+        s.tree_playouts += m->treePlayouts();
     }
     return s;
 }

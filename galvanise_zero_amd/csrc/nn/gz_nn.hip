@@ -50,6 +50,7 @@ struct gz_net {
 
     char* dmem = nullptr;          // all weights, one allocation
     KParams kp{};                  // weight pointers filled in, outputs per launch
+    std::mutex wmu;                // guards dmem / kp's weight pointers / has_weights (weight rolls)
 
     hipStream_t stream = nullptr;  // for the synchronous host-buffer forward
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -399,12 +400,18 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     put(o_vdb, vdb, d.num_values * 4);
 
     HIPCHK(hipSetDevice(net->device));
-    if (net->dmem) { HIPCHK(hipFree(net->dmem)); net->dmem = nullptr; }
-    HIPCHK(hipMalloc((void**)&net->dmem, L.off));
-    HIPCHK(hipMemcpy(net->dmem, img.data(), L.off, hipMemcpyHostToDevice));
-
+    char* m = nullptr;
+    HIPCHK(hipMalloc((void**)&m, L.off));
+    if (hipMemcpy(m, img.data(), L.off, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(m);
+        return fail("weight upload failed");
+    }
+    // swap under the lock launch_segments takes: a launcher thread running a generation roll sees
+    // either the old or the new image, never a mix
+    std::unique_lock<std::mutex> wl(net->wmu);
+    char* old = net->dmem;
+    net->dmem = m;
     KParams& kp = net->kp;
-    char* m = net->dmem;
     kp.w0 = (const __bf16*)(m + o_w0);
     kp.b0 = (const float*)(m + o_b0);
     kp.wres = (const __bf16*)(m + o_wres);
@@ -420,6 +427,11 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     kp.vdw = (const float*)(m + o_vdw);
     kp.vdb = (const float*)(m + o_vdb);
     net->has_weights = true;
+    wl.unlock();
+    if (old) {   // launches already queued may still read the old image
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipFree(old));
+    }
     return 0;
 }
 
@@ -433,8 +445,11 @@ extern "C" int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_
 
 static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* segs, int nseg,
                            hipEvent_t mid = nullptr) {
-    if (!net->has_weights) return fail("weights not set");
     if (nseg < 1 || nseg > kMaxSegments) return fail("segment count out of range (1.." + std::to_string(kMaxSegments) + ")");
+    // the weight image stays valid until this launch is queued (gz_net_set_weights frees a replaced
+    // image only after a device sync)
+    std::lock_guard<std::mutex> wl(net->wmu);
+    if (!net->has_weights) return fail("weights not set");
     KParams kp = net->kp;
     int n = 0;
     for (int i = 0; i < nseg; ++i) {
@@ -494,7 +509,6 @@ static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* se
 
 static int launch(gz_net* net, hipStream_t stream, const float* d_planes, int n,
                   float* const* d_pol, float* d_val) {
-    if (n <= 0) return net->has_weights ? 0 : fail("weights not set");
     gz_segment sg{};
     sg.rows = n;
     sg.planes = d_planes;

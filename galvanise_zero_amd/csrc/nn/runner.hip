@@ -86,6 +86,9 @@ struct gz_runner {
     std::string fail_msg;
     std::mutex sm_;                  // guards sample_json
     std::string sample_json;         // comma-joined sample objects awaiting gz_runner_fetch_samples
+    gz_unique_states* shared_unique = nullptr;   // per_pool_unique_states == 0: one filter for all pools
+    std::atomic<int> live_pools{0};  // pools whose main loop is running (not kDead)
+    bool started = false;
 };
 
 static void set_failed(gz_runner* r, const std::string& msg) {
@@ -134,6 +137,8 @@ static void engine_main(gz_runner* r, int tid) {
             progressed = true;
             if (n <= 0) {                 // main loop ended (never in self-play) or error
                 p.state.store(kDead, std::memory_order_release);
+                r->live_pools.fetch_sub(1, std::memory_order_relaxed);
+                r->qcv.notify_one();
                 if (n < 0) set_failed(r, std::string("gz_pool_poll: ") + gz_engine_last_error());
                 continue;
             }
@@ -241,8 +246,13 @@ static void launcher_main(gz_runner* r) {
             if (min_rows > 0 && !r->queue.empty()) {
                 int queued = 0;
                 for (int i : r->queue) queued += r->pools[i].rows;
+                int inflight_pools = 0;
+                for (int k : inflight) inflight_pools += (int)r->batches_ring[k].pools.size();
+                // no more rows can arrive while every live pool is queued or in flight
+                const bool all_waiting =
+                    (int)r->queue.size() + inflight_pools >= r->live_pools.load(std::memory_order_relaxed);
                 const auto deadline = r->pools[r->queue.front()].queued_at + max_wait;
-                if (queued < min_rows && (int)r->queue.size() < GZ_MAX_SEGMENTS &&
+                if (queued < min_rows && !all_waiting && (int)r->queue.size() < GZ_MAX_SEGMENTS &&
                     std::chrono::steady_clock::now() < deadline) {
                     // wait for more pools, the deadline, or (next loop) the batch in flight
                     r->qcv.wait_until(lk, std::min(deadline, std::chrono::steady_clock::now() +
@@ -346,6 +356,24 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
     const int npools = cfg->num_threads * cfg->pools_per_thread;
     r->pools = std::vector<Pool>(npools);
     const int B = cfg->batch_size;
+    {   // every game coroutine maps its own stack + guard page (2 mappings, engine/coro.cpp)
+        long max_maps = 65530;
+        if (FILE* f = std::fopen("/proc/sys/vm/max_map_count", "r")) {
+            if (std::fscanf(f, "%ld", &max_maps) != 1) max_maps = 65530;
+            std::fclose(f);
+        }
+        const long need = 2L * npools * B + 8192;
+        if (need > max_maps) {
+            g_err = "runner needs about " + std::to_string(need) + " memory mappings for " +
+                    std::to_string((long)npools * B) + " game coroutines, vm.max_map_count is " +
+                    std::to_string(max_maps) + ": use fewer games per GPU";
+            gz_runner_destroy(r);
+            return nullptr;
+        }
+    }
+    if (!cfg->per_pool_unique_states) {
+        r->shared_unique = gz_unique_states_create(sm, t, 1000);   // supervisor.cpp:31
+    }
     size_t out_per_row = num_values;
     for (int i = 0; i < num_policies; ++i) out_per_row += policy_sizes[i];
     for (int i = 0; i < npools; ++i) {
@@ -363,8 +391,8 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
         }
         p.h_val = ho;
         const std::string ident = "gpu" + std::to_string(cfg->device) + "_p" + std::to_string(i);
-        p.pool = gz_pool_create(sm, t, B, ident.c_str(), cfg->seed, cfg->game_index_base + (long)i * B, nullptr,
-                                p.h_planes, p.h_pol.data(), p.h_val);
+        p.pool = gz_pool_create(sm, t, B, ident.c_str(), cfg->seed, cfg->game_index_base + (long)i * B,
+                                r->shared_unique, p.h_planes, p.h_pol.data(), p.h_val);
         if (!p.pool) {
             g_err = std::string("gz_pool_create: ") + gz_engine_last_error();
             gz_runner_destroy(r);
@@ -375,6 +403,14 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
 }
 
 extern "C" int gz_runner_start(gz_runner* r) {
+    // the pools' games are started by their engine threads; a second start would add a second
+    // set of games with the same seeds
+    if (r->started) {
+        g_err = "runner already started (a stopped runner cannot be restarted: create a new one)";
+        return -1;
+    }
+    r->started = true;
+    r->live_pools = (int)r->pools.size();
     r->stop = false;
     r->launcher = std::thread(launcher_main, r);
     for (int i = 0; i < r->cfg.num_threads; ++i) r->threads.emplace_back(engine_main, r, i);
@@ -443,6 +479,7 @@ extern "C" int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out) {
         out->aborts += s.aborts_game_length;
         out->dupes += s.dupes;
         out->completed_game_evals += s.completed_game_evals;
+        out->tree_playouts += s.tree_playouts;
     }
     return r->failed.load() ? -1 : 0;
 }
@@ -476,5 +513,19 @@ extern "C" void gz_runner_destroy(gz_runner* r) {
         if (b.evm) (void)hipEventDestroy(b.evm);
     }
     if (r->stream) (void)hipStreamDestroy(r->stream);
+    gz_unique_states_destroy(r->shared_unique);
     delete r;
+}
+
+// clear_unique_states at a generation roll (supervisor_impl.cpp:138-144, worker.py:160): the
+// shared filter, or every pool's own one (UniqueStates locks, so the engine threads may be running)
+extern "C" int gz_runner_clear_unique_states(gz_runner* r) {
+    if (!r) return -1;
+    if (r->shared_unique) return gz_unique_states_clear(r->shared_unique);
+    for (Pool& p : r->pools)
+        if (p.pool && gz_pool_clear_unique_states(p.pool) != 0) {
+            g_err = gz_engine_last_error();
+            return -1;
+        }
+    return 0;
 }

@@ -10,14 +10,15 @@ from . import _native, cppinterface
 class SelfPlayRunner(object):
     def __init__(self, hip_net, sm, transformer, conf, device=0, num_threads=8, pools_per_thread=2,
                  batch_size=256, seed=0, game_index_base=0, keep_samples=False, max_launch_rows=0,
-                 spin_yield_playouts=0, min_launch_rows=0, max_launch_wait_us=0):
+                 spin_yield_playouts=0, min_launch_rows=0, max_launch_wait_us=0, per_pool_unique_states=True):
         self.lib = _native.runner_lib()
         _native.engine_lib()
         self.net = hip_net
         self.sm = sm
         self.c_transformer = cppinterface.create_c_transformer(transformer)
         self.cfg = _native.GzRunnerConfig(device, num_threads, pools_per_thread, batch_size, seed,
-                                          game_index_base, 1, int(keep_samples), max_launch_rows,
+                                          game_index_base, int(bool(per_pool_unique_states)),
+                                          int(keep_samples), max_launch_rows,
                                           min_launch_rows, max_launch_wait_us)
         self.conf = _native.make_selfplay_config(conf)
         # build extension (engine/config.h): 0 keeps the reference's never-yielding playout loop
@@ -34,7 +35,14 @@ class SelfPlayRunner(object):
         self.batch_size = batch_size
 
     def start(self):
-        self.lib.gz_runner_start(self.handle)
+        if self.lib.gz_runner_start(self.handle) != 0:
+            raise RuntimeError("gz_runner_start: %s" % self.lib.gz_runner_last_error().decode())
+
+    def clear_unique_states(self):
+        """Supervisor.clear_unique_states (supervisor_impl.cpp:138-144) at a generation roll
+        (worker.py:160)."""
+        if self.lib.gz_runner_clear_unique_states(self.handle) != 0:
+            raise RuntimeError("gz_runner_clear_unique_states: %s" % self.lib.gz_runner_last_error().decode())
 
     def wait_batches(self, total, timeout_s=600.0):
         rc = self.lib.gz_runner_wait_batches(self.handle, total, timeout_s)

@@ -95,6 +95,7 @@ typedef struct gz_pool_stats {
     long evaluations;
     long polls;
     long completed_game_evals;   /* NN evaluations consumed by the completed games */
+    long tree_playouts;          /* tree playouts (treePlayout calls), NN-free ones included */
 } gz_pool_stats;
 
 const char* gz_engine_last_error(void);
@@ -166,6 +167,9 @@ int gz_player_root_children(gz_player* p, int* moves, uint32_t* traversals, floa
 /* ---- game pools for the native GPU driver (one SelfPlayManager each) ------------------------ */
 gz_unique_states* gz_unique_states_create(const gz_sm* sm, const gz_transformer* t, int max_num_dupes);
 void gz_unique_states_destroy(gz_unique_states* u);
+/* UniqueStates::clear (clear_unique_states, supervisor_impl.cpp:138-144): a new generation starts
+ * with an empty duplicate filter (worker.py:160). */
+int gz_unique_states_clear(gz_unique_states* u);
 /* planes_buf [batch*total_size], policy_bufs[r] [batch*P_r], value_buf [batch*V] are caller-owned
  * (e.g. pinned host memory); predictions must be written there before gz_pool_poll(pred_count). */
 gz_pool* gz_pool_create(const gz_sm* sm, const gz_transformer* t, int batch_size, const char* identifier,
@@ -175,6 +179,8 @@ void gz_pool_destroy(gz_pool* p);
 int gz_pool_start(gz_pool* p, const gz_selfplay_config* conf);
 int gz_pool_poll(gz_pool* p, int pred_count);   /* returns rows of planes now in planes_buf */
 int gz_pool_get_stats(gz_pool* p, gz_pool_stats* out);
+/* clears the pool's own duplicate filter (no-op for a pool created with a shared one) */
+int gz_pool_clear_unique_states(gz_pool* p);
 char* gz_pool_fetch_samples(gz_pool* p);          /* JSON or NULL; free with gz_free */
 long gz_pool_take_sample_count(gz_pool* p);       /* drops queued samples, returns how many */
 char* gz_pool_fetch_samples_n(gz_pool* p, long* count);  /* as fetch_samples, *count = records */

@@ -51,7 +51,9 @@ void gz_net_destroy(gz_net* net);
  * weight_spec(): Keras storage order, conv HWIO, BN as gamma,beta,mean,var, dense [in][out]). */
 size_t gz_net_weight_count(const gz_net* net);
 
-/* Upload weights from a host float32 blob (BN folded + packed to bf16 on the host). */
+/* Upload weights from a host float32 blob (BN folded + packed to bf16 on the host).  Safe while a
+ * runner is launching on this net (generation roll): launches issued after the call use the new
+ * weights, launches already in flight finish on the old ones, which are freed after a device sync. */
 int gz_net_set_weights(gz_net* net, const float* blob, size_t count);
 
 /* Upload weights from a *device* float32 blob (e.g. after an RCCL broadcast into device memory). */
@@ -127,7 +129,8 @@ typedef struct gz_runner_config {
     int batch_size;              /* games per pool = rows per NN batch */
     unsigned long long seed;
     long game_index_base;        /* global index of the first game (multi-GPU sharding) */
-    int per_pool_unique_states;  /* pools always own their duplicate filter here (deterministic) */
+    int per_pool_unique_states;  /* 1: each pool owns its duplicate filter (deterministic per pool);
+                                    0: one filter shared by every pool (reference, supervisor.cpp:31) */
     int keep_samples;            /* 1: queue samples for gz_runner_fetch_samples; 0: count and drop */
     int max_launch_rows;         /* cap on rows merged into one launch (0: no cap beyond 32 pools) */
     int min_launch_rows;         /* hold a launch until this many rows are queued ... (0: launch at once) */
@@ -153,12 +156,13 @@ typedef struct gz_runner_stats {
     long large_rows;
     double large_trunk_ms;
     double engine_idle_ms;       /* summed over engine threads: time with none of the thread's pools ready */
+    long tree_playouts;          /* tree playouts of all games (NN-free ones = tree_playouts - rows) */
 } gz_runner_stats;
 
 gz_runner* gz_runner_create(gz_net* net, const struct gz_sm* sm, const struct gz_transformer* t,
                             const gz_runner_config* cfg, const struct gz_selfplay_config* conf,
                             const int* policy_sizes, int num_policies, int num_values);
-int gz_runner_start(gz_runner* r);
+int gz_runner_start(gz_runner* r);   /* once per runner: a stopped runner cannot be restarted */
 int gz_runner_wait_batches(gz_runner* r, long total_batches, double timeout_s);
 int gz_runner_wait_rows(gz_runner* r, long total_rows, double timeout_s);
 int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out);
@@ -167,6 +171,9 @@ void gz_runner_destroy(gz_runner* r);
 /* Samples queued since the last call, as one JSON array of datadesc.Sample records
  * (supervisor_impl.cpp:75-118 field names), or NULL when none; free with gz_free. */
 char* gz_runner_fetch_samples(gz_runner* r);
+/* clear_unique_states (supervisor_impl.cpp:138-144) at a generation roll (worker.py:160); safe while
+ * the runner is running. */
+int gz_runner_clear_unique_states(gz_runner* r);
 const char* gz_runner_last_error(void);
 
 #ifdef __cplusplus

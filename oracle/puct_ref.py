@@ -424,6 +424,10 @@ class Evaluator(object):
         # int * float -> float, truncated back to int (evaluator.cpp:782)
         max_non_converged = int(F32(F32(max_evaluations) * F32(conf["evaluation_multiplier_to_convergence"])))
         max_tree_playouts = 4 * max_non_converged
+        # build extension spin_yield_playouts (engine/config.h, evaluator.cpp playoutMain): yield
+        # the coroutine after that many consecutive NN-free playouts; 0 = the reference's loop
+        spin = int(conf.get("spin_yield_playouts", 0) or 0)
+        evals_seen, quiet = self.stats["num_evaluations"], 0
         while True:
             is_converged = self.converged(conf["converged_visits"])
             if self.root.is_finalised and self.stats["num_tree_playouts"] > 100:
@@ -437,6 +441,14 @@ class Evaluator(object):
             if not is_converged and self.stats["num_evaluations"] > max_non_converged:
                 break
             yield from self.tree_playout(self.root, [])
+            if spin > 0:
+                if self.stats["num_evaluations"] != evals_seen:
+                    evals_seen, quiet = self.stats["num_evaluations"], 0
+                else:
+                    quiet += 1
+                    if quiet >= spin:
+                        quiet = 0
+                        yield from self.scheduler.yield_()
 
     # ---- moves (evaluator.cpp:888-1098) -----------------------------------------------------
     def fast_apply_move(self, nxt):

@@ -166,6 +166,42 @@ def test_spin_yield_keeps_each_game_identical(small):
     assert any(x.shape != y.shape or not np.array_equal(x, y) for x, y in zip(log_a, log_b))
 
 
+@pytest.mark.parametrize("spin", [1, 3])
+def test_spin_yield_matches_oracle(small, spin):
+    """The oracle models the spin-yield extension (puct_ref.Evaluator.playout_main): native and
+    oracle stay bit-identical batch by batch with it on, so runner pools (bench default 1000) can
+    be replayed through the oracle exactly (tests/test_runner_gpu.py)."""
+    import attr
+    conf = _selfplay_conf(16, 0.25, False)
+    d = attr.asdict(conf)
+    for k in ("puct_config", "run_to_end_puct_config"):
+        d[k]["spin_yield_playouts"] = spin
+    nlog, nsamples, _, _ = run_native_supervisor(small, d, 4, 900, seed=31)
+    olog, osamples, _ = run_oracle_supervisor(small, d, 4, 900, seed=31, native_log=nlog)
+    assert len(nlog) == len(olog) == 900
+    assert [sample_key(small, s, True) for s in nsamples] == [sample_key(small, s, False) for s in osamples]
+    assert len(nsamples) > 5
+
+
+def test_spin_fast_path_identical():
+    """The root spin fast path (evaluator.cpp spinPlayout: root -> finalised win playouts without the
+    full selection pass) changes nothing: breakthrough 8x8 self-play with it on, off, and on with
+    GZ_VERIFY_FASTPATH=1 (every spin playout re-selected by the ordinary path, abort on mismatch)
+    gives identical samples; the run reaches the multi-win spin (tree playouts >> evaluations)."""
+    import subprocess
+    import sys
+    script = os.path.join(os.path.dirname(__file__), "native", "spin_check.py")
+    outs = []
+    for env in ({"GZ_SPIN_FAST": "0"}, {"GZ_SPIN_FAST": "1"}, {"GZ_SPIN_FAST": "1", "GZ_VERIFY_FASTPATH": "1"}):
+        e = dict(os.environ, **env)
+        r = subprocess.run([sys.executable, script, "breakthrough", "16", "3000", "100"], env=e,
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert outs[0] == outs[1] == outs[2]
+    assert outs[0]["samples"] > 50 and outs[0]["tree_playouts"] > 3 * outs[0]["evaluations"]
+
+
 def test_player_root_latch_bit_exact():
     """Past 1000 root visits the reference's root latch draws the RNG once per reaching child in
     sorted order (evaluator.cpp:461-475); the engine's unsorted fast path must draw identically."""

@@ -9,8 +9,17 @@
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
-#include <random>
 #include <vector>
+
+// synthetic network: a counter hash (splitmix64) instead of a std::mt19937 stream, so the probe's
+// own cost stays small next to the engine's
+static inline uint64_t mix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+static inline float u01(uint64_t k) { return (float)(mix64(k) >> 40) * (1.0f / 16777216.0f); }
 
 static gz_puct_config base_puct(float noise) {
     gz_puct_config c{};
@@ -48,18 +57,19 @@ static void run(int tid, int B, int polls, int evals, int spin) {
     conf.puct_config.spin_yield_playouts = spin;
     conf.run_to_end_puct_config.spin_yield_playouts = spin;
     gz_pool_start(pool, &conf);
-    std::mt19937 rng(1 + tid);
-    std::uniform_real_distribution<float> U(0.f, 1.f);
+    uint64_t ctr = (uint64_t)(tid + 1) << 40;
     int rows = gz_pool_poll(pool, 0);
     long leaves = 0;
+    long tp_prev = 0;
     double tt = 0, worst = 0, win_t = 0;
     long win_l = 0;
     for (int i = 0; i < polls; ++i) {
-        for (int r = 0; r < rows; ++r) {
-            float s0 = 0, s1 = 0;
-            for (int k = 0; k < 155; ++k) { pol0[r * 155 + k] = U(rng); s0 += pol0[r * 155 + k]; pol1[r * 155 + k] = U(rng); s1 += pol1[r * 155 + k]; }
-            for (int k = 0; k < 155; ++k) { pol0[r * 155 + k] /= s0; pol1[r * 155 + k] /= s1; }
-            val[r * 2] = U(rng); val[r * 2 + 1] = 1 - val[r * 2];
+        for (int r = 0; r < rows; ++r) {   // roughly uniform policies, uniform value
+            for (int k = 0; k < 155; ++k) {
+                pol0[r * 155 + k] = (0.5f + u01(ctr++)) * (1.0f / 155);
+                pol1[r * 155 + k] = (0.5f + u01(ctr++)) * (1.0f / 155);
+            }
+            val[r * 2] = u01(ctr++); val[r * 2 + 1] = 1 - val[r * 2];
         }
         auto a = std::chrono::steady_clock::now();
         const int done = rows;
@@ -69,7 +79,11 @@ static void run(int tid, int B, int polls, int evals, int spin) {
         win_t += dt;
         win_l += done;
         if (tid == 0 && (i + 1) % 2000 == 0) {
-            std::printf("thread 0 polls %6d: window %.2f us/leaf\n", i + 1, win_t / win_l * 1e6);
+            gz_pool_stats ws;
+            gz_pool_get_stats(pool, &ws);
+            std::printf("thread 0 polls %6d: window %.2f us/leaf, %.1f tree playouts/leaf, games %ld\n", i + 1,
+                        win_t / win_l * 1e6, (double)(ws.tree_playouts - tp_prev) / win_l, ws.games_completed);
+            tp_prev = ws.tree_playouts;
             std::fflush(stdout);
             win_t = 0;
             win_l = 0;

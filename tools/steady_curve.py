@@ -1,0 +1,65 @@
+"""Self-play throughput over time from the initial position (the approach to steady state): per
+interval leaf-evals/s, games/s, GPU busy and launch size of the native runner on one GPU.
+Usage: python tools/steady_curve.py [--seconds S] [--interval I] [--pools P] [--threads T]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=300)
+    ap.add_argument("--interval", type=float, default=10)
+    ap.add_argument("--pools", type=int, default=2)
+    ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--spin-yield", type=int, default=1000)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    import bench
+    from galvanise_zero_amd._native import HipNet
+    from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS
+    from galvanise_zero_amd.nn.weights import random_weights, to_blob
+    from galvanise_zero_amd.runner import SelfPlayRunner
+    sm, t, desc = bench.setup_game(args.config)
+    net = HipNet(desc, 0)
+    net.set_weights(to_blob(random_weights(desc, 7921)))
+    cpus = len(os.sched_getaffinity(0))
+    threads = args.threads or max(1, min(15, cpus - 1))
+    conf = bench.selfplay_conf("template", BASELINE_CONFIGS[args.config]["evals"])
+    r = SelfPlayRunner(net, sm, t, conf, device=0, num_threads=threads, pools_per_thread=args.pools,
+                       batch_size=args.batch, seed=20251015, spin_yield_playouts=args.spin_yield,
+                       min_launch_rows=1024, max_launch_wait_us=3000)
+    games = threads * args.pools * args.batch
+    r.start()
+    t0 = time.time()
+    prev, tp = r.stats(), t0
+    rows_log = []
+    while time.time() - t0 < args.seconds:
+        time.sleep(args.interval)
+        st, now = r.stats(), time.time()
+        dt = now - tp
+        d = {k: st[k] - prev[k] for k in st}
+        row = {"t": round(now - t0, 1), "evals_per_s": d["rows"] / dt, "games_per_s": d["games_completed"] / dt,
+               "games_total": st["games_completed"], "games_per_slot": st["games_completed"] / games,
+               "gpu_busy": d["kernel_ms"] / 1e3 / dt,
+               "rows_per_launch": d["rows"] / max(1, d["kernel_launches"]),
+               "evals_per_game_cum": st["completed_game_evals"] / max(1, st["games_completed"])}
+        rows_log.append(row)
+        print(json.dumps(row), flush=True)
+        prev, tp = st, now
+    r.stop()
+    r.close()
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump({"threads": threads, "pools_per_thread": args.pools, "games": games, "curve": rows_log}, f)
+
+
+if __name__ == "__main__":
+    main()
