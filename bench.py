@@ -1,28 +1,34 @@
 """Benchmark: self-play games/sec + NN leaf-evals/sec, breakthrough 8x8 @ 800 playouts/move
 (BASELINE.json configs[1]: 6-block x 128-filter net, eval batch 256), on N GPUs of one node.
 
-One process per GPU (torchrun for N>1).  Each rank runs the native self-play runner on its GPU:
-T engine threads x P game pools x 256 games (eval batch 256 per pool, as the reference's
-Supervisor batch_size); one launcher thread merges the pools waiting for predictions into
-segmented launches of the fused HIP forward.  Games shard across ranks by global game index (no
-data-path collective); RCCL is used only to broadcast the weight blob from rank 0 (the
-generation-roll hook) before timing.
+One process per GPU.  `python bench.py --gpus N` with N > 1 (and no WORLD_SIZE in the environment)
+starts N ranks itself (torch.distributed.run, before any GPU call) and exits with their status;
+under torchrun each rank reads RANK / LOCAL_RANK / WORLD_SIZE.  Each rank pins itself to its share
+of the process's CPUs and runs the native self-play runner on its GPU: T engine threads x P game
+pools x 256 games (eval batch 256 per pool, as the reference's Supervisor batch_size); one launcher
+thread merges the pools waiting for predictions into segmented launches of the fused HIP forward.
+Games shard across ranks by global game index (no data-path collective); RCCL is used only to
+broadcast the weight blob from rank 0 (the generation-roll hook) before timing.
 
-A "step" = one eval batch (256 leaf evaluations) for every pool of the rank, i.e. T*P*256 leaf
-evaluations.  W warmup steps, then exactly K timed steps bracketed by barrier + synchronize; the
-time is the max over ranks, `value` is whole-job leaf-evals/sec.  Rank 0 prints one JSON line.
+Steady state.  Every game starts from the initial position, and what a leaf costs the host depends
+on the game phase (endgames spin through up to millions of NN-free playouts per move), so a
+window right after the start measures the opening only, and no game completes in it.  The bench
+therefore first AGES the game population: it runs self-play until the population has turned over
+(--age-games: completed games per game slot, default 1.0) or --age-seconds elapse, so the timed
+window sees games of every age, as a self-play worker does after its first minutes
+(profiles/r02*_curve* show the approach to steady state).
 
-Every game starts from the initial position and the per-leaf host cost grows as games reach their
-endgames (the reference's playout loop re-selects finalised children for up to millions of
-playouts per move there), so the rate depends on the window.  The default window (W=100, K=10000
-steps = 143M leaf evaluations at 14 threads x 4 pools) runs from ~1 s to ~150 s after the start and
-covers the first generation of games reaching their endgames; `--steps` larger measures further
-into the steady state (DESIGN.md section 6 lists measured long-run rates).
+A "step" = --step-rows leaf evaluations (default 2^19) per rank.  W warmup steps, then exactly K
+timed steps bracketed by barrier + synchronize; the time is the max over ranks; `value` is
+whole-job leaf-evals/sec and `games_per_sec` the games completed in the window per second.
+Rank 0 prints one JSON line.
 """
 import argparse
 import json
 import os
 import resource
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,15 +37,13 @@ sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0      # gfx950 dense bf16 MFMA (MI355X_MICROARCH.md)
 # L2-served read rate per CU (MI355X_MICROARCH.md "Indexed rows: gather into LDS": rows shared by
-# every workgroup, 66-73 GB/s per CU, 16.8-18.8 TB/s chip-wide).  Every trunk workgroup streams the
-# whole conv weight image from its XCD's L2, so below ~1.5 boards per CU the trunk is bound by this
-# rate, not by the MFMA peak.
+# every workgroup, 66-73 GB/s per CU).  Every trunk workgroup streams the whole conv weight image
+# from its XCD's L2.
 PEAK_L2_GBPS_PER_CU = 70.0
 NUM_CUS = 256
 # PMC-measured fabric bytes per trunk launch (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE,
-# separate rocprofv3 --pmc passes of tools/gpu_pmc.sh at 256 / 640 rows, profiles/r01k_pmc.txt).
-# PMC counters cannot be read inside the timed run, so the measured per-launch figure of the same
-# kernel at the bench's launch size is reported.
+# separate rocprofv3 --pmc passes, tools/gpu_pmc.sh).  PMC counters cannot be read inside the timed
+# run, so the figure measured for the same kernel is reported with its source.
 TRAFFIC_PER_LAUNCH = {"gznn::trunk_kernel<128, 8, 8, 1, 1>": (14290.1 * 2 + 320.0) * 1024,
                       "gznn::trunk_kernel<128, 8, 8, 2, 1>": (14722.3 * 2 + 800.0) * 1024}
 TRAFFIC_SOURCE = "profiles/r01k_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 256- and 640-row launches)"
@@ -48,22 +52,28 @@ TRAFFIC_SOURCE = "profiles/r01k_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10000)
-    ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--threads", type=int, default=0, help="host threads per GPU (0: auto)")
-    ap.add_argument("--pools", type=int, default=4, help="game pools per thread")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--step-rows", type=int, default=1 << 19, help="leaf evaluations per step per rank")
+    ap.add_argument("--age-games", type=float, default=1.0,
+                    help="steady state: age the game population until this many games per game slot completed ...")
+    ap.add_argument("--age-seconds", type=float, default=300.0, help="... or this many seconds passed (0: no aging)")
+    ap.add_argument("--threads", type=int, default=0, help="engine threads per GPU (0: the rank's CPUs - 1, max 31)")
+    ap.add_argument("--pools", type=int, default=2, help="game pools per engine thread")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--evals", type=int, default=0, help="evals per move (0: the config's, 800 for cfg2)")
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
                     help="BASELINE.json configs[i-1]; 2 (breakthrough 8x8, 6x128) is the headline workload, "
                          "3-5 (reversi 10x128, hexLG13 12x256, amazons_10x10 20x256) run the same path")
     ap.add_argument("--mode", choices=["template", "literal"], default="template")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--min-launch-rows", type=int, default=1024,
-                    help="hold a launch (while one is in flight) until this many rows are queued ...")
+                    help="hold a launch until this many rows are queued ...")
     ap.add_argument("--max-launch-wait-us", type=int, default=3000, help="... or its oldest pool waited this long")
+    ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for CPU-side tests)")
+    ap.add_argument("--device", type=int, default=-1, help="GPU of every rank (-1: LOCAL_RANK; tests share one GPU)")
     ap.add_argument("--spin-yield", type=int, default=1000,
                     help="yield a game's coroutine after this many NN-free playouts (0: reference behaviour)")
     return ap.parse_args()
@@ -96,53 +106,97 @@ def setup_game(config=2):
     return sm, transformer, desc
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds, evals, mode, batch, config=2):
-    """CPU restatement timed on the host: the same engine driven by the reference's Python poll
-    loop with the oracle's CPU forward (oracle/nn_ref.py) in place of the GPU."""
-    import numpy as np
-    from threadpoolctl import threadpool_limits
+    """The reference's CPU self-play design timed on this host: cppinterface.Supervisor with C++
+    worker threads (2 pools of `batch` games each, supervisor.cpp:79-99,196-245) running the tree
+    search while the Python poll loop (cppinterface.py:131-144) runs the network on the CPU
+    (float32 torch, all the rank's cores: oracle/nn_torch.py) -- the same engine and workload as the
+    GPU run, only the network moves to the host."""
+    import torch
     from galvanise_zero_amd import cppinterface
     from galvanise_zero_amd.nn.weights import random_weights
-    from oracle import nn_ref
+    from oracle.nn_torch import TorchCPUNet
 
     sm, transformer, desc = setup_game(config)
-    weights = random_weights(desc, 7921)
-    cores = min(16, os.cpu_count() or 1)
-
-    class OracleModel(object):
-        def predict_on_batch(self, X):
-            return nn_ref.forward(desc, weights, X)
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    workers = max(1, cores // 4)
+    model = TorchCPUNet(desc, random_weights(desc, 7921))
 
     class NN(object):
         gdl_bases_transformer = transformer
 
         def get_model(self):
-            return OracleModel()
+            return model
 
-    with threadpool_limits(limits=cores):
-        sup = cppinterface.Supervisor(sm, NN(), batch_size=batch, seed=1, per_pool_unique_states=True)
-        sup.start_self_play(selfplay_conf(mode, evals), 0)
-        t0 = time.time()
+    sup = cppinterface.Supervisor(sm, NN(), batch_size=batch, seed=1, per_pool_unique_states=True)
+    sup.start_self_play(selfplay_conf(mode, evals), workers)
+    t_end = time.time() + min(5.0, seconds / 4)          # warm the pools (first batches, torch init)
+    while time.time() < t_end:
         sup.poll(do_stats=True)
-        rows0 = sup.total_predictions
-        t0 = time.time()
-        while time.time() - t0 < seconds:
-            sup.poll(do_stats=True)
-        el = time.time() - t0
-        rows = sup.total_predictions - rows0
+    rows0 = sup.total_predictions
+    t0 = time.time()
+    while time.time() - t0 < seconds:
+        sup.poll(do_stats=True)
+    el = time.time() - t0
+    rows = sup.total_predictions - rows0
     return {"value": rows / el, "unit": "leaf-evals/s", "cores": cores, "kind": "port",
-            "sample": "%.1f s of %s self-play (%d games inline, batch %d, %d evals/move, %s mode): "
-                      "native engine + oracle fp64 numpy forward via the Python poll loop" %
-                      (el, sm.game, batch, batch, evals, mode)}
+            "cpu_model": cpu_model(),
+            "sample": "%.1f s of %s self-play from the initial position (%d evals/move, %s mode): the reference's "
+                      "worker-thread design (%d C++ worker threads x 2 pools x %d games, Supervisor.poll loop) with "
+                      "a float32 torch-CPU network on %d threads" % (el, sm.game, evals, mode, workers, batch, cores)}
+
+
+def launch_ranks(args):
+    """--gpus N without a process group: start N ranks (one per GPU) with torch.distributed.run
+    before anything touches the GPU, and exit with their status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def pin_rank_cpus(local_rank, local_world):
+    """Split this process's CPUs into contiguous per-rank shares (ranks of one node start with the
+    same affinity); returns the CPU count this rank may use."""
+    if not hasattr(os, "sched_getaffinity"):
+        return os.cpu_count() or 4
+    cpus = sorted(os.sched_getaffinity(0))
+    if local_world > 1 and len(cpus) >= 2 * local_world:
+        share = len(cpus) // local_world
+        mine = cpus[local_rank * share:(local_rank + 1) * share]
+        os.sched_setaffinity(0, mine)
+        return len(mine)
+    return len(cpus)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != args.gpus:
+        print("[bench] note: --gpus %d but WORLD_SIZE %d; using the process group" % (args.gpus, world),
+              file=sys.stderr)
+    cpus = pin_rank_cpus(local_rank, local_world)
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -151,14 +205,18 @@ def main():
     from galvanise_zero_amd.runner import SelfPlayRunner
     from galvanise_zero_amd import shard
 
-    torch.cuda.set_device(local_rank)
+    device = local_rank if args.device < 0 else args.device
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(args.backend)
 
     from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS
     evals = args.evals or BASELINE_CONFIGS[args.config]["evals"]
     sm, transformer, desc = setup_game(args.config)
-    net = HipNet(desc, local_rank)
+    net = HipNet(desc, device)
 
     # weights: rank 0 creates, RCCL broadcast of the blob (the only collective on the path)
     blob = torch.empty(net.weight_count, dtype=torch.float32, device="cuda")
@@ -167,26 +225,22 @@ def main():
     shard.broadcast_weights(blob, src=0)
     torch.cuda.synchronize()
     net.set_weights_device(blob.data_ptr(), net.weight_count)
+    blob_sum = float(blob.double().sum().item())
 
-    # the CPUs this process may run on (the GPU box pins 16 per GPU; os.cpu_count() is the machine)
-    cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 4)
-    if world > 1 and cpus >= (os.cpu_count() or cpus):   # unpinned ranks share the machine
-        cpus = cpus // world
-    threads = args.threads or max(1, min(15, cpus - 1))   # + the launcher (mostly asleep) and main
-    runner = SelfPlayRunner(net, sm, transformer, selfplay_conf(args.mode, evals), device=local_rank,
+    threads = args.threads or max(1, min(31, cpus - 1))   # + the launcher (mostly asleep) and main
+    games_per_rank = threads * args.pools * args.batch
+    game_base = shard.game_index_base(rank, games_per_rank)
+    runner = SelfPlayRunner(net, sm, transformer, selfplay_conf(args.mode, evals), device=device,
                             num_threads=threads, pools_per_thread=args.pools, batch_size=args.batch,
-                            seed=args.seed,
-                            game_index_base=shard.game_index_base(rank, threads * args.pools * args.batch),
+                            seed=args.seed, game_index_base=game_base,
                             spin_yield_playouts=args.spin_yield, min_launch_rows=args.min_launch_rows,
                             max_launch_wait_us=args.max_launch_wait_us)
-    npools = runner.num_pools
 
     def barrier():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
 
-    rows_per_step = npools * args.batch
     t_start = time.perf_counter()
 
     def heartbeat(st):
@@ -196,27 +250,49 @@ def main():
               file=sys.stderr, flush=True)
 
     runner.start()
-    runner.wait_rows(args.warmup * rows_per_step, timeout_s=3600, progress=heartbeat)
+    # ---- aging: until the population has turned over (or the time limit) ----------------------
+    age_target = args.age_games * games_per_rank
+    while args.age_seconds > 0:
+        st = runner.stats()
+        el = time.perf_counter() - t_start
+        if st["games_completed"] >= age_target or el >= args.age_seconds:
+            break
+        runner.wait_rows(st["rows"] + (1 << 18), timeout_s=600)
+        if int(el) // 10 != int(time.perf_counter() - t_start) // 10:
+            heartbeat(runner.stats())
+    aged = runner.stats()
+    age_s = time.perf_counter() - t_start
+    # ---- warmup + timed steps --------------------------------------------------------------------
+    rows_base = aged["rows"]
+    runner.wait_rows(rows_base + args.warmup * args.step_rows, timeout_s=3600, progress=heartbeat)
     barrier()
     s0 = runner.stats()
     t0 = time.perf_counter()
-    runner.wait_rows((args.warmup + args.steps) * rows_per_step, timeout_s=3600, progress=heartbeat)
+    runner.wait_rows(s0["rows"] + args.steps * args.step_rows, timeout_s=3600, progress=heartbeat)
     s1 = runner.stats()
     t1 = time.perf_counter()
     barrier()
-    t_end = time.perf_counter()
     runner.stop()
     elapsed = t1 - t0
 
     d = {k: s1[k] - s0[k] for k in s1}
+    # every rank's global game range (disjoint by construction; checked here)
+    ranges = [(game_base, game_base + games_per_rank)]
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, ranges[0])
+        ranges = allr
+    disjoint = all(a[1] <= b[0] for a, b in zip(sorted(ranges), sorted(ranges)[1:]))
     totals, T = shard.reduce_counters(
         [d["rows"], d["batches"], d["games_completed"], d["games_with_samples"], d["samples"], d["kernel_ms"],
-         d["kernel_launches"], d["segments"], s1["games_completed"], s1["completed_game_evals"], d["trunk_ms"],
+         d["kernel_launches"], d["segments"], d["completed_game_evals"], d["trunk_ms"],
          d["large_launches"], d["large_rows"], d["large_trunk_ms"], d["engine_idle_ms"],
-         d["no_samples"], d["resigns"], d["aborts"], d["dupes"]],
+         d["no_samples"], d["resigns"], d["aborts"], d["dupes"], d["tree_playouts"],
+         aged["games_completed"], games_per_rank, blob_sum],
         elapsed, device="cuda")
-    (rows, batches, games, games_s, samples, kms, launches, segments, games_all, game_evals_all, tms,
-     l_launches, l_rows, l_tms, idle_ms, no_samples, resigns, aborts, dupes) = totals
+    (rows, batches, games, games_s, samples, kms, launches, segments, game_evals, tms,
+     l_launches, l_rows, l_tms, idle_ms, no_samples, resigns, aborts, dupes, tree_playouts,
+     aged_games, games_total, blob_sums) = totals
 
     if rank == 0:
         flops = desc.flops_per_eval()
@@ -251,14 +327,16 @@ def main():
             "value": rows / T,
             "unit": "leaf-evals/s",
             "games_per_sec": games / T,
-            # mean NN evaluations of the games completed since start (biased to short games early on)
-            "evals_per_completed_game": game_evals_all / games_all if games_all else None,
-            "games_completed_total": games_all,
+            "evals_per_completed_game": game_evals / games if games else None,
             "sample_games_per_sec": games_s / T,
             "samples_per_sec": samples / T,
             # selfplaymanager.cpp:161-200 counters over the window
-            "selfplay_counters": {"no_sample_games": no_samples, "resigns": resigns, "aborts": aborts,
-                                  "duplicate_states": dupes},
+            "selfplay_counters": {"games_completed": games, "no_sample_games": no_samples, "resigns": resigns,
+                                  "aborts": aborts, "duplicate_states": dupes},
+            "nn_free_playouts_per_leaf": (tree_playouts - rows) / rows if rows else None,
+            "steady_state": {"aging_s": age_s, "games_completed_before_window": aged_games,
+                             "games_per_slot_before_window": aged_games / games_total if games_total else None,
+                             "age_games_target": args.age_games, "age_seconds_limit": args.age_seconds},
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -271,11 +349,17 @@ def main():
             "config": {"workload": "%s self-play (BASELINE configs[%d]), v1 %dx%d net, %d evals/move (%s mode), "
                                    "eval batch %d" % (sm.game, args.config - 1, desc.residual_layers,
                                                       desc.cnn_filter_size, evals, args.mode, args.batch),
-                       "games_per_gpu": npools * args.batch, "threads_per_gpu": threads,
+                       "step": "%d leaf evaluations per rank" % args.step_rows,
+                       "games_per_gpu": games_per_rank, "threads_per_gpu": threads, "cpus_per_gpu": cpus,
                        "pools_per_thread": args.pools, "eval_batch": args.batch,
-                       "launch_batching": {"min_rows": args.min_launch_rows, "max_wait_us": args.max_launch_wait_us}, "parallelism": "games sharded dp%d" % world},
+                       "launch_batching": {"min_rows": args.min_launch_rows, "max_wait_us": args.max_launch_wait_us},
+                       "parallelism": "games sharded dp%d" % world,
+                       "game_ranges": {"per_rank": ranges, "disjoint": disjoint},
+                       "weights_broadcast": {"collective": "RCCL broadcast" if world > 1 else "none (1 rank)",
+                                             "identical_on_all_ranks": abs(blob_sums - world * blob_sum) <= 1e-6 * max(1.0, abs(world * blob_sum))}},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_BF16_TFLOPS, "traffic": TRAFFIC_PER_LAUNCH.get(dom) if args.config == 2 else None,
+                         "frac": achieved / PEAK_BF16_TFLOPS,
+                         "traffic": TRAFFIC_PER_LAUNCH.get(dom) if args.config == 2 else None,
                          "traffic_unit": "bytes/launch",
                          "traffic_source": TRAFFIC_SOURCE if args.config == 2 and dom in TRAFFIC_PER_LAUNCH else None,
                          "kernel": dom, "avg_kernel_ms": per_variant[dom]["avg_kernel_ms"] if dom else None,
@@ -292,10 +376,11 @@ def main():
         }
         if dom:
             out["roofline"]["l2_weight_stream"] = per_variant[dom]["l2_weight_stream"]
+    runner.close()   # frees the games' trees before the CPU baseline
+    if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, evals, args.mode, args.batch, args.config)
         print(json.dumps(out), flush=True)
-    runner.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -53,7 +53,12 @@ class GzNetDesc(ctypes.Structure):
                 ("flatten_nchw", ctypes.c_int),
                 ("conv_bias", ctypes.c_int),
                 ("value_bn", ctypes.c_int),
-                ("value_sigmoid", ctypes.c_int)]
+                ("value_sigmoid", ctypes.c_int),
+                ("precision", ctypes.c_int)]
+
+GZ_PRECISION_BF16 = 1
+GZ_PRECISION_SPLIT = 3
+PRECISIONS = {"bf16": GZ_PRECISION_BF16, "fp32": GZ_PRECISION_SPLIT}
 
 
 _FP = ctypes.POINTER(ctypes.c_float)
@@ -95,8 +100,9 @@ def nn_lib():
     return lib
 
 
-def make_net_desc(desc):
+def make_net_desc(desc, precision=GZ_PRECISION_BF16):
     d = GzNetDesc()
+    d.precision = precision
     d.input_channels = desc.input_channels
     d.input_columns = desc.input_columns
     d.input_rows = desc.input_rows
@@ -121,12 +127,15 @@ def _fptr(a):
 
 
 class HipNet(object):
-    """Owner of a gz_net handle: the MI355X forward of one network on one device."""
+    """Owner of a gz_net handle: the MI355X forward of one network on one device.
+    precision: "bf16" (bf16 operands) or "fp32" (split hi/lo bf16 operands, three MFMAs per product:
+    fp32-class accuracy, include/gzero_nn.h GZ_PRECISION_SPLIT)."""
 
-    def __init__(self, desc, device=0):
+    def __init__(self, desc, device=0, precision="bf16"):
         self.lib = nn_lib()
         self.desc = desc
-        self._cdesc = make_net_desc(desc)
+        self.precision = precision
+        self._cdesc = make_net_desc(desc, PRECISIONS[precision])
         self.handle = self.lib.gz_net_create(ctypes.byref(self._cdesc), device)
         if not self.handle:
             raise RuntimeError("gz_net_create failed: %s" % self.lib.gz_nn_last_error().decode())

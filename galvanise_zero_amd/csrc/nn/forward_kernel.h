@@ -57,9 +57,10 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 struct KParams {
-    const __bf16* w0;        // initial conv, packed [K0/32][F][32]
+    const __bf16* w0;        // initial conv, packed [K0/32][F][32] (split precision: the hi parts)
+    const __bf16* w0lo;      // split precision: the lo parts, same layout
     const float* b0;         // [F]
-    const __bf16* wres;      // trunk convs, packed [2B][9][F/32][F][32]
+    const __bf16* wres;      // trunk convs, packed [2B][9][F/32][F][32] (split: [..][F][hi 32 | lo 32])
     const float* bres;       // [2B][F]
     const float* wh;         // head 1x1 convs (BN folded) [2R+1][F]
     const float* bh;         // [2R+1]
@@ -91,23 +92,30 @@ __host__ __device__ constexpr int ring_depth(int nst, int ks, int ct, int cap) {
     return 1;
 }
 
-template <int F, int H, int W, int NB = 1>
+// P = 1: bf16 operands.  P = 3: split precision ("fp32 accuracy"): every fp32 operand x is carried
+// as x_hi = bf16(x), x_lo = bf16(x - x_hi) and each product as hi*hi + hi*lo + lo*hi (three MFMAs,
+// fp32 accumulation): ~16 significant bits per operand instead of 8.
+template <int F, int H, int W, int NB = 1, int P = 1>
 struct Geo {
+    static constexpr int P2 = P == 3 ? 2 : 1;        // bf16 parts per operand
     static constexpr int NPOS = H * W;
     static constexpr int PT = (NPOS + 15) / 16;      // position tiles per board (MFMA N)
     static constexpr int TT = NB * PT;               // position tiles per wave (all boards)
     static constexpr int CT = F / 64;                // co tiles per wave (MFMA M)
     static constexpr int KC = F / 32;                // k-steps per tap
     static constexpr int CPR = F / 8;                // 16-byte chunks of channels per row
-    static constexpr int ROWS = ((CPR + 14) * 16 + 255) & ~255;   // LDS row stride (rotated chunks)
+    static constexpr int HALF = ((CPR + 14) * 16 + 255) & ~255;   // one part's rotated chunks
+    static constexpr int ROWS = P2 * HALF;           // LDS row stride: hi part, then lo part
     static constexpr int ACT_BYTES = (NPOS + 1) * ROWS;           // + one all-zero row
     // k-steps per ring stage and the ring's VGPR budget: F = 256 (4 co tiles per wave, 16 weight
     // VGPRs per k-step) streams single k-steps through a 64-VGPR ring so the accumulators, the
     // residual and the B fragments still fit the 512 registers of a wave without spilling
-    static constexpr int KS = CT >= 4 ? 1 : 2;
+    static constexpr int KS = (CT >= 4 || P2 == 2) ? 1 : 2;
+    static constexpr int NFR = CT * P2;              // weight fragments per k-step per lane
+    static constexpr int ROWB = 64 * P2;             // bytes per output channel per k-step
     static constexpr int NST = 9 * KC / KS;          // ring stages per conv
-    static constexpr int R = ring_depth(NST, KS, CT, CT >= 4 ? 64 : 96);
-    static constexpr int LPS = KS * CT;              // weight loads per stage per lane
+    static constexpr int R = ring_depth(NST, KS, NFR, CT >= 4 ? 64 : 96);
+    static constexpr int LPS = KS * NFR;             // weight loads per stage per lane
     // Single-image mode: when two ping-pong images (+ bias table) do not fit the 160 KB of LDS
     // (F = 256 on 10x10 / 13x13 boards), one image is overwritten in place: every conv's MFMAs
     // finish reading it (barrier) before its epilogue writes it.  The input staging and head
@@ -118,6 +126,7 @@ struct Geo {
     // registers, lane-contiguous (one coalesced 1 KB store / load per wave and tile).
     static constexpr bool RG = CT * TT * 4 * 2 > 256;
     static_assert(F % 64 == 0, "filters must be a multiple of 64");
+    static_assert(P == 1 || (P == 3 && NB == 1 && CT <= 2), "split precision: F <= 128, one board per workgroup");
     static_assert(!SI || NB == 1, "single-image mode takes one board per workgroup");
     static_assert(!RG || SI, "the global residual is implemented for single-image kernels");
     static constexpr int RESID_BYTES = RG ? 4 * CT * TT * 64 * 16 : 0;   // per workgroup
@@ -130,8 +139,8 @@ __device__ __forceinline__ int swz(int q) { return (2 * q) & 14; }
 
 // LDS bytes of the trunk kernel beyond the two activation image sets: bias table + scratch
 // (input staging / 1x1-head partials; the scratch aliases the second image set).
-__host__ __device__ inline int trunk_scratch_bytes(int npos, int C, int K0, int R) {
-    const int in_stage = align16(C * npos * 4) + align16((npos + 1) * K0 * 2);
+__host__ __device__ inline int trunk_scratch_bytes(int npos, int C, int K0, int R, int P2 = 1) {
+    const int in_stage = align16(C * npos * 4) + P2 * align16((npos + 1) * K0 * 2);
     const int hc = 2 * R + 1;
     const int heads = align16(4 * hc * npos * 4);
     return in_stage > heads ? in_stage : heads;
@@ -147,14 +156,23 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
     return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
 }
 
-template <int F, int H, int W>
+__device__ __forceinline__ float bf16_lo(float x) { return x - (float)(__bf16)x; }
+
+template <int F, int H, int W, int P = 1>
 __device__ __forceinline__ void store_act(char* X, int p, int co, f32x4 v) {
-    using G = Geo<F, H, W>;
+    using G = Geo<F, H, W, 1, P>;
     if (p < G::NPOS) {
+        char* a = X + p * G::ROWS + (((co >> 3) + swz(p)) << 4) + (co & 7) * 2;
         uint2 u;
         u.x = pack2(v[0], v[1]);
         u.y = pack2(v[2], v[3]);
-        *(uint2*)(X + p * G::ROWS + (((co >> 3) + swz(p)) << 4) + (co & 7) * 2) = u;
+        *(uint2*)a = u;
+        if constexpr (G::P2 == 2) {    // the lo part, same chunk of the row's second half
+            uint2 l;
+            l.x = pack2(bf16_lo(v[0]), bf16_lo(v[1]));
+            l.y = pack2(bf16_lo(v[2]), bf16_lo(v[3]));
+            *(uint2*)(a + G::HALF) = l;
+        }
     }
 }
 
@@ -192,10 +210,10 @@ __device__ __forceinline__ void ring_ready(bf16x8& v) { asm volatile("" : "+v"(v
 
 // ---- trunk -------------------------------------------------------------------------------------
 
-template <int F, int H, int W, int NB>
+template <int F, int H, int W, int NB, int P>
 struct Ring {
-    using G = Geo<F, H, W, NB>;
-    bf16x8 r[G::R][G::KS][G::CT];
+    using G = Geo<F, H, W, NB, P>;
+    bf16x8 r[G::R][G::KS][G::NFR];    // fragment f = ct * P2 + part
 };
 
 // Issue stage `gs` of the trunk weight stream (clamped to the last stage) into ring slot SLOT.
@@ -205,22 +223,28 @@ struct Ring {
 // copies values between VGPRs and AGPRs freely: an inline-asm load's destination could be copied
 // (or its register reused) before the data lands.  They issue the ring with ordinary loads, which
 // the compiler tracks (it places the waits and never copies an in-flight register).
-template <int F, int H, int W, int NB, int SLOT, int... CTS>
-__device__ __forceinline__ void ring_issue_k(Ring<F, H, W, NB>& ring, int k, uint32_t woff, const char* sb,
-                                             std::integer_sequence<int, CTS...>) {
-    if constexpr (Geo<F, H, W, NB>::SI)
-        ((ring.r[SLOT][k][CTS] = *(const bf16x8*)(sb + woff + CTS * 16 * 64)), ...);
+// byte offset of weight fragment f (= ct * P2 + part) within a k-step, relative to the lane's row
+template <int P2, int ROWB, int FR>
+struct FragOff {
+    static constexpr int value = (FR / P2) * 16 * ROWB + (FR % P2) * 64;
+};
+template <int F, int H, int W, int NB, int P, int SLOT, int... FRS>
+__device__ __forceinline__ void ring_issue_k(Ring<F, H, W, NB, P>& ring, int k, uint32_t woff, const char* sb,
+                                             std::integer_sequence<int, FRS...>) {
+    using G = Geo<F, H, W, NB, P>;
+    if constexpr (G::SI)
+        ((ring.r[SLOT][k][FRS] = *(const bf16x8*)(sb + woff + FragOff<G::P2, G::ROWB, FRS>::value)), ...);
     else
-        ((ring.r[SLOT][k][CTS] = gload_issue<CTS * 16 * 64>(woff, sb)), ...);
+        ((ring.r[SLOT][k][FRS] = gload_issue<FragOff<G::P2, G::ROWB, FRS>::value>(woff, sb)), ...);
 }
-template <int F, int H, int W, int NB, int SLOT>
-__device__ __forceinline__ void ring_issue(Ring<F, H, W, NB>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
-    using G = Geo<F, H, W, NB>;
+template <int F, int H, int W, int NB, int P, int SLOT>
+__device__ __forceinline__ void ring_issue(Ring<F, H, W, NB, P>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
+    using G = Geo<F, H, W, NB, P>;
     const int s = gs < gmax ? gs : gmax;
 #pragma unroll
     for (int k = 0; k < G::KS; ++k)
-        ring_issue_k<F, H, W, NB, SLOT>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * 64,
-                                        std::make_integer_sequence<int, G::CT>{});
+        ring_issue_k<F, H, W, NB, P, SLOT>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * G::ROWB,
+                                           std::make_integer_sequence<int, G::NFR>{});
 }
 
 // LDS byte offset (within a board image) of a lane's B fragment for tap `tap`, position tile pt,
@@ -230,9 +254,9 @@ __device__ __forceinline__ void ring_issue(Ring<F, H, W, NB>& ring, const __bf16
 __device__ __forceinline__ void launder(int& v) { asm volatile("" : "+v"(v)); }
 template <typename T>
 __device__ __forceinline__ void launder_ptr(T*& p) { asm volatile("" : "+v"(p)); }
-template <int F, int H, int W>
+template <int F, int H, int W, int P = 1>
 __device__ __forceinline__ int tap_base(int tap, int pt, int lane) {
-    using G = Geo<F, H, W>;
+    using G = Geo<F, H, W, 1, P>;
     const int li = lane & 15, g = lane >> 4;
     const int dy = tap / 3 - 1, dx = tap % 3 - 1;
     const int p = 16 * pt + li;
@@ -245,21 +269,21 @@ __device__ __forceinline__ int tap_base(int tap, int pt, int lane) {
 // One 3x3 'same' conv over the NB LDS images at X (board b at X + b*ACT_BYTES):
 // acc[ct][t] = W * X (fp32 accumulate), tile t = b*PT + pt.  gs0 = global stage index of this
 // conv's first stage; on entry stages gs0 .. gs0+R-2 are in flight in ring slots 0..R-2.
-template <int F, int H, int W, int NB, int ST>
-__device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, H, W, NB>& ring,
-                                           f32x4 (&acc)[Geo<F, H, W, NB>::CT][Geo<F, H, W, NB>::TT],
-                                           bf16x8 (&b)[2][Geo<F, H, W, NB>::TT], const __bf16* wres, uint32_t woff,
-                                           int gs0, int gmax, int& lane) {
-    using G = Geo<F, H, W, NB>;
-    constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC;
+template <int F, int H, int W, int NB, int P, int ST>
+__device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, H, W, NB, P>& ring,
+                                           f32x4 (&acc)[Geo<F, H, W, NB, P>::CT][Geo<F, H, W, NB, P>::TT],
+                                           bf16x8 (&b)[2][Geo<F, H, W, NB, P>::TT][Geo<F, H, W, NB, P>::P2],
+                                           const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane) {
+    using G = Geo<F, H, W, NB, P>;
+    constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC, P2 = G::P2;
     // refill the slot stage ST-1 consumed with stage ST+R-1, then wait for stage ST
-    ring_issue<F, H, W, NB, (ST + R - 1) % R>(ring, wres, woff, gs0 + ST + R - 1, gmax);
+    ring_issue<F, H, W, NB, P, (ST + R - 1) % R>(ring, wres, woff, gs0 + ST + R - 1, gmax);
     if constexpr (!G::SI) {
         ring_wait<(R - 1) * G::LPS>();
 #pragma unroll
         for (int k = 0; k < KS; ++k)
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) ring_ready(ring.r[ST % R][k][ct]);
+            for (int f = 0; f < G::NFR; ++f) ring_ready(ring.r[ST % R][k][f]);
     }
 
 #pragma unroll
@@ -271,72 +295,85 @@ __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, H
             if (kc == 0) launder(lane);
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) {
-                const char* a = X + tap_base<F, H, W>(tap, pt, lane) + kc * 64;
+                const char* a = X + tap_base<F, H, W, P>(tap, pt, lane) + kc * 64;
 #pragma unroll
-                for (int bb = 0; bb < NB; ++bb) b[jn & 1][bb * PT + pt] = *(const bf16x8*)(a + bb * G::ACT_BYTES);
+                for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+                    for (int h = 0; h < P2; ++h)
+                        b[jn & 1][bb * PT + pt][h] = *(const bf16x8*)(a + bb * G::ACT_BYTES + h * G::HALF);
             }
         }
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-            for (int t = 0; t < TT; ++t)
-                acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring.r[ST % R][k][ct], b[j & 1][t], acc[ct][t], 0, 0, 0);
+            for (int t = 0; t < TT; ++t) {
+                const bf16x8 w_hi = ring.r[ST % R][k][ct * P2];
+                acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[j & 1][t][0], acc[ct][t], 0, 0, 0);
+                if constexpr (P2 == 2) {   // split precision: + hi*lo + lo*hi
+                    const bf16x8 w_lo = ring.r[ST % R][k][ct * P2 + 1];
+                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[j & 1][t][1], acc[ct][t], 0, 0, 0);
+                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[j & 1][t][0], acc[ct][t], 0, 0, 0);
+                }
+            }
         // interleave the next k-step's B reads with this k-step's MFMAs (CT MFMAs, one ds_read,
         // ...) instead of the compiler's cluster of reads ahead of the MFMA run: measured 2-4 %
         // faster at 640-1024 rows, neutral at 256 (same-box A/B, profiles/r01l_interleave_ab.txt)
         if constexpr (!G::SI) {
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
-                __builtin_amdgcn_sched_group_barrier(0x008, CT, 0);   // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // DS read
+                __builtin_amdgcn_sched_group_barrier(0x008, CT * (P2 == 2 ? 3 : 1), 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, P2, 0);                       // DS read
             }
         }
     }
 }
 
-template <int F, int H, int W, int NB, int... S>
-__device__ __forceinline__ void ring_prime(Ring<F, H, W, NB>& ring, const __bf16* wres, uint32_t woff, int gmax,
+template <int F, int H, int W, int NB, int P, int... S>
+__device__ __forceinline__ void ring_prime(Ring<F, H, W, NB, P>& ring, const __bf16* wres, uint32_t woff, int gmax,
                                            std::integer_sequence<int, S...>) {
-    (ring_issue<F, H, W, NB, S>(ring, wres, woff, S, gmax), ...);
+    (ring_issue<F, H, W, NB, P, S>(ring, wres, woff, S, gmax), ...);
 }
 
-template <int F, int H, int W, int NB, int... ST>
-__device__ __forceinline__ void conv_stages(const char* __restrict__ X, Ring<F, H, W, NB>& ring,
-                                            f32x4 (&acc)[Geo<F, H, W, NB>::CT][Geo<F, H, W, NB>::TT],
-                                            bf16x8 (&b)[2][Geo<F, H, W, NB>::TT], const __bf16* wres,
-                                            uint32_t woff, int gs0, int gmax, int& lane,
+template <int F, int H, int W, int NB, int P, int... ST>
+__device__ __forceinline__ void conv_stages(const char* __restrict__ X, Ring<F, H, W, NB, P>& ring,
+                                            f32x4 (&acc)[Geo<F, H, W, NB, P>::CT][Geo<F, H, W, NB, P>::TT],
+                                            bf16x8 (&b)[2][Geo<F, H, W, NB, P>::TT][Geo<F, H, W, NB, P>::P2],
+                                            const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane,
                                             std::integer_sequence<int, ST...>) {
-    (conv_stage<F, H, W, NB, ST>(X, ring, acc, b, wres, woff, gs0, gmax, lane), ...);
+    (conv_stage<F, H, W, NB, P, ST>(X, ring, acc, b, wres, woff, gs0, gmax, lane), ...);
 }
 
-template <int F, int H, int W, int NB>
-__device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, H, W, NB>& ring,
-                                        f32x4 (&acc)[Geo<F, H, W, NB>::CT][Geo<F, H, W, NB>::TT],
+template <int F, int H, int W, int NB, int P>
+__device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, H, W, NB, P>& ring,
+                                        f32x4 (&acc)[Geo<F, H, W, NB, P>::CT][Geo<F, H, W, NB, P>::TT],
                                         const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane) {
-    using G = Geo<F, H, W, NB>;
+    using G = Geo<F, H, W, NB, P>;
     constexpr int PT = G::PT, TT = G::TT;
 #pragma unroll
     for (int ct = 0; ct < G::CT; ++ct)
 #pragma unroll
         for (int t = 0; t < TT; ++t) acc[ct][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 b[2][TT];
+    bf16x8 b[2][TT][G::P2];
     // k-step 0 = tap 0 (dy = dx = -1), kc 0
     launder(lane);
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt) {
-        const char* a = X + tap_base<F, H, W>(0, pt, lane);
+        const char* a = X + tap_base<F, H, W, P>(0, pt, lane);
 #pragma unroll
-        for (int bb = 0; bb < NB; ++bb) b[0][bb * PT + pt] = *(const bf16x8*)(a + bb * G::ACT_BYTES);
+        for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+            for (int h = 0; h < G::P2; ++h) b[0][bb * PT + pt][h] = *(const bf16x8*)(a + bb * G::ACT_BYTES + h * G::HALF);
     }
-    conv_stages<F, H, W, NB>(X, ring, acc, b, wres, woff, gs0, gmax, lane, std::make_integer_sequence<int, G::NST>{});
+    conv_stages<F, H, W, NB, P>(X, ring, acc, b, wres, woff, gs0, gmax, lane, std::make_integer_sequence<int, G::NST>{});
 }
 
 // NB boards per workgroup of 4 waves; WPE = minimum resident waves per SIMD the register
 // allocation must allow (amdgpu_waves_per_eu), i.e. WPE workgroups per CU.
-template <int F, int H, int W, int NB, int WPE>
+template <int F, int H, int W, int NB, int WPE, int P>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 trunk_kernel(const KParams kp) {
-    using G = Geo<F, H, W, NB>;
+    using G = Geo<F, H, W, NB, P>;
+    constexpr int P2 = G::P2;
     constexpr int NPOS = G::NPOS, PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, kThreads = 256;
     constexpr int ACT = G::ACT_BYTES;
 
@@ -359,10 +396,10 @@ trunk_kernel(const KParams kp) {
     const int C = kp.C, K0 = kp.K0;
 
     // prime the weight ring: stages 0 .. R-2 of the trunk stream
-    const uint32_t woff = (uint32_t)((co_base + li) * 64 + 16 * g);   // lane's fragment bytes within a k-step
+    const uint32_t woff = (uint32_t)((co_base + li) * G::ROWB + 16 * g);   // lane's fragment bytes within a k-step
     const int gmax = 2 * kp.B * G::NST - 1;
-    Ring<F, H, W, NB> ring;
-    if (kp.B > 0) ring_prime<F, H, W, NB>(ring, kp.wres, woff, gmax, std::make_integer_sequence<int, R - 1>{});
+    Ring<F, H, W, NB, P> ring;
+    if (kp.B > 0) ring_prime<F, H, W, NB, P>(ring, kp.wres, woff, gmax, std::make_integer_sequence<int, R - 1>{});
 
     f32x4 acc[CT][TT];
     f32x4 resid[RG ? 1 : CT][RG ? 1 : TT];
@@ -379,6 +416,7 @@ trunk_kernel(const KParams kp) {
     float* sin = (float*)SCR;
     char* IM = SCR + align16(C * NPOS * 4);
     const int imrow = K0 * 2;
+    char* IMlo = IM + align16((NPOS + 1) * imrow);   // split precision: lo parts of the inputs
     const int imswz = ((K0 >> 3) < 16 ? (K0 >> 3) : 16) - 1;
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
@@ -389,7 +427,7 @@ trunk_kernel(const KParams kp) {
         __syncthreads();
         // IM[p][k], k = tap*C + c, zero padded to K0: zero the image, then one thread per
         // (position, tap) copies its C channels (compile-time divisors only)
-        for (int i = tid; i < (NPOS + 1) * K0 / 8; i += kThreads) ((uint4*)IM)[i] = uint4{0u, 0u, 0u, 0u};
+        for (int i = tid; i < P2 * align16((NPOS + 1) * imrow) / 16; i += kThreads) ((uint4*)IM)[i] = uint4{0u, 0u, 0u, 0u};
         __syncthreads();
         for (int i = tid; i < NPOS * 9; i += kThreads) {
             const int p = i / 9, tap = i - (i / 9) * 9;
@@ -398,7 +436,10 @@ trunk_kernel(const KParams kp) {
                 const float* src = sin + y * W + x;
                 for (int c = 0; c < C; ++c) {
                     const int k = tap * C + c;
-                    *(__bf16*)(IM + p * imrow + ((((k >> 3) ^ (p & imswz))) << 4) + (k & 7) * 2) = (__bf16)src[c * NPOS];
+                    const int o = p * imrow + ((((k >> 3) ^ (p & imswz))) << 4) + (k & 7) * 2;
+                    const float v = src[c * NPOS];
+                    *(__bf16*)(IM + o) = (__bf16)v;
+                    if constexpr (P2 == 2) *(__bf16*)(IMlo + o) = (__bf16)bf16_lo(v);
                 }
             }
         }
@@ -409,19 +450,29 @@ trunk_kernel(const KParams kp) {
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) acc[ct][bb * PT + pt] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int s = 0; s < (K0 >> 5); ++s) {
-            bf16x8 a[CT];
+            bf16x8 a[CT], alo[CT];
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct)
-                a[ct] = *(const bf16x8*)(kp.w0 + ((size_t)(s * F + co_base + 16 * ct + li)) * 32 + 8 * g);
+            for (int ct = 0; ct < CT; ++ct) {
+                const size_t o = ((size_t)(s * F + co_base + 16 * ct + li)) * 32 + 8 * g;
+                a[ct] = *(const bf16x8*)(kp.w0 + o);
+                if constexpr (P2 == 2) alo[ct] = *(const bf16x8*)(kp.w0lo + o);
+            }
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) {
                 const int p = 16 * pt + li;
                 const int q = p < NPOS ? p : NPOS;
-                const bf16x8 bq = *(const bf16x8*)(IM + q * imrow + ((((s * 4 + g)) ^ (q & imswz)) << 4));
+                const int o = q * imrow + ((((s * 4 + g)) ^ (q & imswz)) << 4);
+                const bf16x8 bq = *(const bf16x8*)(IM + o);
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct)
-                    acc[ct][bb * PT + pt] =
-                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], bq, acc[ct][bb * PT + pt], 0, 0, 0);
+                for (int ct = 0; ct < CT; ++ct) {
+                    f32x4& c = acc[ct][bb * PT + pt];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], bq, c, 0, 0, 0);
+                    if constexpr (P2 == 2) {
+                        const bf16x8 bql = *(const bf16x8*)(IMlo + o);
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], bql, c, 0, 0, 0);
+                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[ct], bq, c, 0, 0, 0);
+                    }
+                }
             }
         }
         if constexpr (SI) __syncthreads();    // the image overwrites the im2col scratch
@@ -439,7 +490,7 @@ trunk_kernel(const KParams kp) {
                 if constexpr (RG) rg[(ct * TT + bb * PT + pt) * 64] = v;
                 else resid[ct][bb * PT + pt] = v;
                 acc[ct][bb * PT + pt] = v;    // the heads read acc when there is no residual block
-                store_act<F, H, W>(X0 + bb * ACT, 16 * pt + li, co, v);
+                store_act<F, H, W, P>(X0 + bb * ACT, 16 * pt + li, co, v);
             }
         }
         __syncthreads();    // scratch is reused by the next board
@@ -457,7 +508,7 @@ trunk_kernel(const KParams kp) {
         for (int cv = 0; cv < 2 * kp.B; ++cv) {
             const bool second = cv & 1;
             const float* bt = btab + cv * F;
-            conv3x3<F, H, W, NB>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane);
+            conv3x3<F, H, W, NB, P>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane);
             __syncthreads();    // every wave has finished reading the image it is about to overwrite
             // residual tile addresses are formed here, not hoisted out of the loop (44 x 64-bit)
             f32x4* rgc = rg;
@@ -485,7 +536,7 @@ trunk_kernel(const KParams kp) {
                         else resid[ct][t] = v;
                         acc[ct][t] = v;
                     }
-                    store_act<F, H, W>(X0, 16 * t + li, co, v);
+                    store_act<F, H, W, P>(X0, 16 * t + li, co, v);
                 }
             }
             __syncthreads();
@@ -495,7 +546,7 @@ trunk_kernel(const KParams kp) {
         const float* b_a = btab + (2 * blk) * F;
         const float* b_b = b_a + F;
 
-        conv3x3<F, H, W, NB>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane);
+        conv3x3<F, H, W, NB, P>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -507,12 +558,12 @@ trunk_kernel(const KParams kp) {
                 v[1] = act_fn(v[1] + bias.y, kp.leaky);
                 v[2] = act_fn(v[2] + bias.z, kp.leaky);
                 v[3] = act_fn(v[3] + bias.w, kp.leaky);
-                store_act<F, H, W>(X1 + (t / PT) * ACT, 16 * (t % PT) + li, co, v);
+                store_act<F, H, W, P>(X1 + (t / PT) * ACT, 16 * (t % PT) + li, co, v);
             }
         }
         __syncthreads();
 
-        conv3x3<F, H, W, NB>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane);
+        conv3x3<F, H, W, NB, P>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -527,7 +578,7 @@ trunk_kernel(const KParams kp) {
                 v[3] = act_fn(v[3] + bias.w + r[3], kp.leaky);
                 resid[ct][t] = v;
                 acc[ct][t] = v;
-                store_act<F, H, W>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v);
+                store_act<F, H, W, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v);
             }
         }
         __syncthreads();
@@ -540,7 +591,7 @@ trunk_kernel(const KParams kp) {
 #pragma unroll
             for (int k = 0; k < G::KS; ++k)
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct) ring_ready(ring.r[s][k][ct]);
+                for (int f = 0; f < G::NFR; ++f) ring_ready(ring.r[s][k][f]);
     }
 
     GZ_STAMP(2);

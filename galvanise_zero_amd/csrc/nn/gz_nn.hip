@@ -46,6 +46,7 @@ struct gz_net {
         int resid_bytes = 0;       // global residual scratch per workgroup
     } small, large;                // launches below / from large_min_rows rows
     int large_min_rows = 1 << 30;
+    int p2 = 1;                    // bf16 parts per operand: 1 (bf16) or 2 (split precision)
     bool has_weights = false;
 
     char* dmem = nullptr;          // all weights, one allocation
@@ -82,19 +83,27 @@ struct KernelChoice {
     int resid_bytes = 0;           // global residual scratch per workgroup (0: registers)
 };
 
-template <int F, int H, int W, int NB, int WPE>
+template <int F, int H, int W, int NB, int WPE, int P = 1>
 static KernelChoice kernel_for() {
     KernelChoice k;
-    k.fn = (const void*)&trunk_kernel<F, H, W, NB, WPE>;
-    k.act_bytes = Geo<F, H, W, NB>::ACT_BYTES;
+    k.fn = (const void*)&trunk_kernel<F, H, W, NB, WPE, P>;
+    k.act_bytes = Geo<F, H, W, NB, P>::ACT_BYTES;
     k.nb = NB;
-    k.single_image = Geo<F, H, W, NB>::SI;
-    k.resid_bytes = Geo<F, H, W, NB>::RESID_BYTES;
+    k.single_image = Geo<F, H, W, NB, P>::SI;
+    k.resid_bytes = Geo<F, H, W, NB, P>::RESID_BYTES;
     return k;
 }
 
 template <int F, int H, int W>
-static KernelChoice variants(int v) {
+static KernelChoice variants(int v, int precision) {
+    if (precision == GZ_PRECISION_SPLIT) {
+        // split precision: hi + lo images, one board per workgroup (LDS), F <= 128
+        if constexpr (F <= 128) {
+            if constexpr (2 * Geo<F, H, W, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024)
+                return v == 11 ? kernel_for<F, H, W, 1, 1, 3>() : KernelChoice{};
+        }
+        return KernelChoice{};
+    }
     if constexpr (4 * Geo<F, H, W, 1>::ACT_BYTES + 16 * 1024 > 160 * 1024) {   // large boards / filters: one board per workgroup only
         return v == 11 ? kernel_for<F, H, W, 1, 1>() : KernelChoice{};
     } else switch (v) {
@@ -115,9 +124,9 @@ static KernelChoice variants(int v) {
 constexpr int kSmallVariant = 11, kLargeVariant = 21, kLargeMinRows = 257;
 constexpr int kCUs = 256;
 
-static KernelChoice select_kernel(int F, int H, int W, int v) {
+static KernelChoice select_kernel(int F, int H, int W, int v, int precision) {
 #define GZ_CASE(F_, H_, W_) \
-    if (F == F_ && H == H_ && W == W_) return variants<F_, H_, W_>(v);
+    if (F == F_ && H == H_ && W == W_) return variants<F_, H_, W_>(v, precision);
     GZ_CASE(64, 6, 6)
     GZ_CASE(128, 6, 6)
     GZ_CASE(64, 8, 8)
@@ -155,26 +164,30 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     if (d.cnn_kernel_size != 3) { fail("only cnn_kernel_size 3 is supported"); return nullptr; }
     if (d.role_count < 1 || d.role_count > GZ_MAX_ROLES) { fail("role_count out of range"); return nullptr; }
     if (d.num_values < 1 || d.num_values > 4) { fail("num_values out of range"); return nullptr; }
+    const int precision = d.precision == 0 ? GZ_PRECISION_BF16 : d.precision;
+    if (precision != GZ_PRECISION_BF16 && precision != GZ_PRECISION_SPLIT) { fail("unknown precision"); return nullptr; }
     int vs = kSmallVariant, vl = kLargeVariant, min_large = kLargeMinRows;
     if (const char* e = getenv("GZ_KERNEL_VARIANT")) {   // experiments: one fixed variant
         vs = vl = atoi(e);
         min_large = 1 << 30;
     }
-    const KernelChoice kc = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vs);
-    KernelChoice kl = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vl);
+    const KernelChoice kc = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vs, precision);
+    KernelChoice kl = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vl, precision);
     if (kc.fn && !kl.fn && vl != vs) {   // geometries with a single (one board per workgroup) variant
         kl = kc;
         min_large = 1 << 30;
     }
     if (!kc.fn || !kl.fn) {
         fail("unsupported network geometry F=" + std::to_string(d.cnn_filter_size) + " H=" +
-             std::to_string(d.input_columns) + " W=" + std::to_string(d.input_rows));
+             std::to_string(d.input_columns) + " W=" + std::to_string(d.input_rows) +
+             (precision == GZ_PRECISION_SPLIT ? " (split precision)" : ""));
         return nullptr;
     }
     gz_net* net = new gz_net;
     net->d = d;
     net->device = device;
     net->large_min_rows = min_large;
+    net->p2 = precision == GZ_PRECISION_SPLIT ? 2 : 1;
     net->K0 = ((9 * d.input_channels + 31) / 32) * 32;
     net->nweights = spec_count(d);
     int maxP = 0;
@@ -182,7 +195,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     const int npos = d.input_columns * d.input_rows;
     // LDS: two ping-pong activation images per board; the scratch (input staging, heads) aliases
     // the second image set, which holds nothing live at those times.
-    const int scr = trunk_scratch_bytes(npos, d.input_channels, net->K0, d.role_count);
+    const int scr = trunk_scratch_bytes(npos, d.input_channels, net->K0, d.role_count, net->p2);
     auto trunk = [&](const KernelChoice& c) {
         gz_net::Trunk t;
         t.fn = c.fn;
@@ -288,9 +301,18 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     const float eps = 1e-3f;
 
     // host images
-    std::vector<uint16_t> w0((size_t)K0 * F, 0);
+    const int P2 = net->p2;
+    std::vector<uint16_t> w0((size_t)K0 * F, 0), w0lo(P2 == 2 ? (size_t)K0 * F : 0, 0);
     std::vector<float> b0(F);
-    std::vector<uint16_t> wres((size_t)2 * B * 9 * F * F);
+    std::vector<uint16_t> wres((size_t)P2 * 2 * B * 9 * F * F);
+    // split precision: x = hi + lo, hi = bf16(x), lo = bf16(x - hi)
+    auto lo_of = [](float v) {
+        const uint16_t h = f2bf(v);
+        uint32_t u = (uint32_t)h << 16;
+        float hf;
+        std::memcpy(&hf, &u, 4);
+        return f2bf(v - hf);
+    };
     std::vector<float> bres((size_t)2 * B * F);
     std::vector<float> wh((size_t)HC * F), bh(HC, 0.f);
 
@@ -321,20 +343,24 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
                 const int tap = k / C, c = k % C;
                 const float v = w[((size_t)tap * C + c) * F + co] * s[co];
                 w0[((size_t)(k / 32) * F + co) * 32 + (k % 32)] = f2bf(v);
+                if (P2 == 2) w0lo[((size_t)(k / 32) * F + co) * 32 + (k % 32)] = lo_of(v);
             }
         }
     }
-    for (int conv = 0; conv < 2 * B; ++conv) {  // [3][3][F][F] -> [tap][kc][co][32]
+    // [3][3][F][F] -> [tap][kc][co][32] (split precision: [tap][kc][co][hi 32 | lo 32])
+    for (int conv = 0; conv < 2 * B; ++conv) {
         const float* w = cur.take((size_t)9 * F * F);
         const float* cb = conv_bias(F);
         bn_fold(F, s, bb, cb);
-        uint16_t* dst = wres.data() + (size_t)conv * 9 * F * F;
+        uint16_t* dst = wres.data() + (size_t)P2 * conv * 9 * F * F;
         for (int co = 0; co < F; ++co) {
             bres[(size_t)conv * F + co] = bb[co];
             for (int tap = 0; tap < 9; ++tap)
                 for (int ci = 0; ci < F; ++ci) {
                     const float v = w[((size_t)tap * F + ci) * F + co] * s[co];
-                    dst[(((size_t)tap * KC + ci / 32) * F + co) * 32 + (ci % 32)] = f2bf(v);
+                    const size_t o = ((((size_t)tap * KC + ci / 32) * F + co) * P2) * 32 + (ci % 32);
+                    dst[o] = f2bf(v);
+                    if (P2 == 2) dst[o + 32] = lo_of(v);
                 }
         }
     }
@@ -370,7 +396,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
 
     // device layout
     Layout L;
-    const size_t o_w0 = L.alloc(w0.size() * 2), o_b0 = L.alloc(b0.size() * 4);
+    const size_t o_w0 = L.alloc(w0.size() * 2), o_w0lo = L.alloc(std::max<size_t>(w0lo.size(), 1) * 2);
+    const size_t o_b0 = L.alloc(b0.size() * 4);
     const size_t o_wres = L.alloc(wres.size() * 2), o_bres = L.alloc(bres.size() * 4);
     const size_t o_wh = L.alloc(wh.size() * 4), o_bh = L.alloc(bh.size() * 4);
     size_t o_pd[GZ_MAX_ROLES], o_pb[GZ_MAX_ROLES];
@@ -384,6 +411,7 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     std::vector<char> img(L.off, 0);
     auto put = [&](size_t off, const void* src, size_t bytes) { std::memcpy(img.data() + off, src, bytes); };
     put(o_w0, w0.data(), w0.size() * 2);
+    if (P2 == 2) put(o_w0lo, w0lo.data(), w0lo.size() * 2);
     put(o_b0, b0.data(), b0.size() * 4);
     put(o_wres, wres.data(), wres.size() * 2);
     put(o_bres, bres.data(), bres.size() * 4);
@@ -413,6 +441,7 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     net->dmem = m;
     KParams& kp = net->kp;
     kp.w0 = (const __bf16*)(m + o_w0);
+    kp.w0lo = (const __bf16*)(m + o_w0lo);
     kp.b0 = (const float*)(m + o_b0);
     kp.wres = (const __bf16*)(m + o_wres);
     kp.bres = (const float*)(m + o_bres);

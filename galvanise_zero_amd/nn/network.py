@@ -23,10 +23,10 @@ def desc_from_conf(nn_model_conf, generation_descr=None):
 class HipModel(object):
     """Model object with the Keras inference surface the hot path uses."""
 
-    def __init__(self, desc, weights, device=0):
+    def __init__(self, desc, weights, device=0, precision="bf16"):
         self.desc = desc
         self.weights = weights
-        self.net = HipNet(desc, device)
+        self.net = HipNet(desc, device, precision)
         self.net.set_weights(to_blob(weights))
 
     def predict_on_batch(self, X):

@@ -39,7 +39,16 @@ typedef struct gz_net_desc {
     int conv_bias;                            /* every Conv2D has use_bias: a bias after each kernel */
     int value_bn;                             /* BatchNormalization after the value head's 1x1 conv  */
     int value_sigmoid;                        /* value Dense activation sigmoid (else softmax)      */
+    /* Arithmetic of the residual trunk (build extension; the reference runs fp32 TF kernels):
+     *   GZ_PRECISION_BF16 (0 or 1): bf16 operands, fp32 accumulation and residual stream;
+     *   GZ_PRECISION_SPLIT (3): fp32 accuracy -- each fp32 operand as bf16 hi + bf16 lo and each
+     *   product as hi*hi + hi*lo + lo*hi on the MFMA (~16 significant bits per operand, fp32
+     *   accumulation); F <= 128.  The heads are fp32 in both modes. */
+    int precision;
 } gz_net_desc;
+
+#define GZ_PRECISION_BF16 1
+#define GZ_PRECISION_SPLIT 3
 
 typedef struct gz_net gz_net;
 

@@ -129,3 +129,68 @@ def test_kernel_variants_identical(variant, hip_device, monkeypatch):
     vnet, _ = _net(desc, 5, hip_device)
     for a, b in zip(base, vnet.forward(x)):
         assert np.array_equal(a, b)
+
+
+# ---- fp32-accuracy mode (split hi/lo bf16 operands, three MFMAs per product) ------------------
+# Stated tolerance against the float64 oracle (reference semantics), per output element and per
+# row (KL divergence of each policy / value row from the oracle's):
+TOL_FP32 = (1e-3, 1e-5)          # max |err|, mean |err| -- set from the measured errors
+TOL_FP32_KL = 1e-6               # max over rows of KL(oracle || kernel)
+SPLIT = ["cfg1", "cfg2", "cfg3", "b0_8x8", "leaky_v3_8x8", "nchw_6x6", "legacy_v1_8x8", "x6_102_json"]
+
+
+def _net_p(desc, seed, device, name, precision):
+    from galvanise_zero_amd._native import HipNet
+    w = random_weights(desc, seed, bias_std=0.2, res_gamma=0.15 if name in DEEP else 1.0)
+    net = HipNet(desc, device, precision)
+    net.set_weights(to_blob(w))
+    return net, w
+
+
+def _kl(ref, got):
+    r = np.clip(ref.astype(np.float64), 1e-30, None)
+    g = np.clip(got.astype(np.float64), 1e-30, None)
+    return float((r * np.log(r / g)).sum(axis=1).max())
+
+
+@pytest.mark.parametrize("name", SPLIT)
+def test_forward_parity_fp32(name, hip_device):
+    desc = VARIANTS[name]
+    net, w = _net_p(desc, 7919, hip_device, name, "fp32")
+    for n in (1, 7, 64):
+        x = random_planes(desc, n, 100 + n)
+        got = net.forward(x)
+        ref = nn_ref.forward(desc, w, x)
+        for i, (g, r) in enumerate(zip(got, ref)):
+            er = _err(g, r)
+            sig = desc.value_sigmoid and i == len(got) - 1
+            kl = 0.0 if sig else _kl(r, g)
+            print("fp32 %s n=%d out%d  vs_ref max %.3g mean %.3g kl %.3g" % (name, n, i, er[0], er[1], kl))
+            assert er[0] <= TOL_FP32[0] and er[1] <= TOL_FP32[1], (name, n, i, er)
+            assert kl <= TOL_FP32_KL, (name, n, i, kl)
+
+
+def test_fp32_tolerance_detects_one_bf16_ulp(hip_device):
+    """The fp32-mode tolerance is tight enough to see a one-bf16-ulp (2^-8 relative) change of
+    one residual block's conv weights."""
+    from galvanise_zero_amd._native import HipNet
+    desc = VARIANTS["cfg2"]
+    w = random_weights(desc, 7919, bias_std=0.2)
+    wp = [(k, v * np.float32(1 + 2.0 ** -8) if k == "res2_conv1" else v) for k, v in w]
+    net = HipNet(desc, hip_device, "fp32")
+    net.set_weights(to_blob(wp))
+    x = random_planes(desc, 64, 164)
+    errs = [_err(g, r)[0] for g, r in zip(net.forward(x), nn_ref.forward(desc, w, x))]
+    print("one-ulp perturbation: max errors", errs)
+    assert max(errs) > TOL_FP32[0]
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2"])
+def test_batch_invariance_fp32(name, hip_device):
+    desc = VARIANTS[name]
+    net, _ = _net_p(desc, 3, hip_device, name, "fp32")
+    x = random_planes(desc, 300, 9)
+    full = net.forward(x)
+    perm = np.random.default_rng(0).permutation(300)[:37]
+    for a, b in zip(full, net.forward(x[perm])):
+        assert np.array_equal(a[perm], b)

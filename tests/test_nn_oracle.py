@@ -126,3 +126,15 @@ def test_arch_fixture_shapes():
                 assert info["input_shape"] == [d.input_channels, d.input_columns, d.input_rows]
                 assert info["policy_units"] == d.policy_dist_count
                 assert all(abs(e - 1e-3) < 1e-12 for e in info["bn_epsilon"])
+
+
+@pytest.mark.parametrize("desc", VARIANTS)
+def test_torch_cpu_fp32_matches_oracle(desc):
+    """oracle/nn_torch.py (bench.py's CPU-baseline network, float32 torch-CPU) agrees with the
+    float64 oracle to float32 accuracy."""
+    from oracle.nn_torch import TorchCPUNet
+    w = random_weights(desc, 3)
+    x = random_planes(desc, 9, 4)
+    for a, b in zip(TorchCPUNet(desc, w).predict_on_batch(x), nn_ref.forward(desc, w, x)):
+        assert a.dtype == np.float32 and a.shape == b.shape
+        assert float(np.abs(a - b).max()) < 2e-5

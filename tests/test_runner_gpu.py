@@ -127,10 +127,11 @@ def _suffix(s):
 
 CASES = {
     # BASELINE configs[1]: breakthrough 8x8 on the 6-block x 128-filter net (the headline workload)
-    "breakthrough_cfg2": (2, "breakthrough", 1200, (0, 7, 13, 19)),
+    "breakthrough_cfg2": (2, "breakthrough", 32, 10, 1200, (0, 7, 13, 19)),
     # BASELINE configs[2]: reversi 8x8 with the draw head (3 values), 10-block x 128-filter net
-    # (reversi games last ~60 moves of >= 16 evaluations: more polls for finished games)
-    "reversi_cfg3": (3, "reversi", 3000, (0, 13)),
+    # (reversi games last ~60 moves of >= 16 evaluations, and the oracle is slow on reversi: pools
+    # of 16 games, 20 per thread -- still 640 rows, up to 512 merged)
+    "reversi_cfg3": (3, "reversi", 16, 20, 1600, (0, 27)),
 }
 
 
@@ -144,7 +145,7 @@ def test_native_runner_matches_oracle(case, hip_device):
     every runner sample of those pools must be identical to the oracle's."""
     from galvanise_zero_amd.runner import SelfPlayRunner
     from oracle import puct_ref as P
-    cfg, game, polls, check_pools = CASES[case]
+    cfg, game, B, ppt, polls, check_pools = CASES[case]
     desc = BASELINE_CONFIGS[cfg]["desc"]
     setup = Setup(game, draw_head=desc.num_values == 3)
     t = setup.transformer
@@ -152,7 +153,7 @@ def test_native_runner_matches_oracle(case, hip_device):
         (desc.input_channels, desc.input_columns, desc.input_rows, list(desc.policy_dist_count), desc.num_values)
     net = _net(desc, 7921, hip_device)
     conf = _runner_conf(8)
-    seed, B, threads, ppt, spin = 20251015, 32, 2, 10, 1000
+    seed, threads, spin = 20251015, 2, 1000
     r = SelfPlayRunner(net, setup.sm, t, conf, device=hip_device, num_threads=threads, pools_per_thread=ppt,
                        batch_size=B, seed=seed, keep_samples=True, spin_yield_playouts=spin,
                        min_launch_rows=512, max_launch_wait_us=2000)
@@ -178,9 +179,11 @@ def test_native_runner_matches_oracle(case, hip_device):
                         "t", seed, pool * B, list(t.policy_dist_count), t.num_rewards, setup.num_prev_states)
         man.start(ocfg)
         pred = (0, [np.zeros(0, np.float32)] * setup.sm.role_count, np.zeros(0, np.float32))
-        for _ in range(3 * polls):
+        for it in range(3 * polls):
             if len(man.samples) >= len(mine):
                 break
+            if it % 200 == 0:
+                print("oracle pool %d poll %d: %d/%d samples" % (pool, it, len(man.samples), len(mine)), flush=True)
             buf = man.poll(*pred)
             assert buf is not None
             x = buf.reshape(-1, t.num_channels, t.num_cols, t.num_rows)
