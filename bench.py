@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--age-games", type=float, default=1.0,
                     help="steady state: age the game population until this many games per game slot completed ...")
     ap.add_argument("--age-seconds", type=float, default=300.0, help="... or this many seconds passed (0: no aging)")
-    ap.add_argument("--threads", type=int, default=0, help="engine threads per GPU (0: the rank's CPUs - 1, max 31)")
+    ap.add_argument("--threads", type=int, default=0, help="engine threads per GPU (0: the rank's CPU share - 1)")
     ap.add_argument("--pools", type=int, default=2, help="game pools per engine thread")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--evals", type=int, default=0, help="evals per move (0: the config's, 800 for cfg2)")
@@ -129,9 +129,9 @@ def cpu_baseline(seconds, evals, mode, batch, config=2):
     from oracle.nn_torch import TorchCPUNet
 
     sm, transformer, desc = setup_game(config)
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cores = cpu_share()
     torch.set_num_threads(cores)
-    workers = max(1, cores // 4)
+    workers = max(1, cores // 8)   # the network, not the tree search, is the CPU cost here
     model = TorchCPUNet(desc, random_weights(desc, 7921))
 
     class NN(object):
@@ -170,18 +170,51 @@ def launch_ranks(args):
     return subprocess.call(cmd)
 
 
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup (v2 cpu.max / v1 cfs quota), or None when unlimited: a container
+    may see every CPU of the host in its affinity mask but be throttled to a share of them (the
+    GPU box: 256 CPUs visible, 16 granted)."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as f:
+                text = f.read().strip()
+        except OSError:
+            continue
+        if parse is not None:
+            quota, period = parse(text)
+            if quota == "max":
+                return None
+            return max(1, int(int(quota) // int(period)))
+        quota = int(text)
+        if quota <= 0:
+            return None
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            return max(1, quota // int(f.read().strip()))
+    return None
+
+
+def cpu_share(local_world=1):
+    """CPUs this rank may use: the affinity mask, capped by the cgroup quota, split over the ranks
+    of the node."""
+    cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 4)
+    quota = cgroup_cpu_quota()
+    if quota is not None:
+        cpus = min(cpus, quota)
+    return max(1, cpus // max(1, local_world))
+
+
 def pin_rank_cpus(local_rank, local_world):
     """Split this process's CPUs into contiguous per-rank shares (ranks of one node start with the
-    same affinity); returns the CPU count this rank may use."""
-    if not hasattr(os, "sched_getaffinity"):
-        return os.cpu_count() or 4
-    cpus = sorted(os.sched_getaffinity(0))
-    if local_world > 1 and len(cpus) >= 2 * local_world:
-        share = len(cpus) // local_world
-        mine = cpus[local_rank * share:(local_rank + 1) * share]
-        os.sched_setaffinity(0, mine)
-        return len(mine)
-    return len(cpus)
+    same affinity) when the node's ranks see more CPUs than their quota share; returns the CPU count
+    this rank may use."""
+    share = cpu_share(local_world)
+    if hasattr(os, "sched_getaffinity") and local_world > 1:
+        cpus = sorted(os.sched_getaffinity(0))
+        if len(cpus) >= share * local_world:
+            per = len(cpus) // local_world
+            os.sched_setaffinity(0, cpus[local_rank * per:(local_rank + 1) * per])
+    return share
 
 
 def main():
@@ -227,7 +260,7 @@ def main():
     net.set_weights_device(blob.data_ptr(), net.weight_count)
     blob_sum = float(blob.double().sum().item())
 
-    threads = args.threads or max(1, min(31, cpus - 1))   # + the launcher (mostly asleep) and main
+    threads = args.threads or max(1, cpus - 1)   # + the launcher (mostly asleep) and main
     games_per_rank = threads * args.pools * args.batch
     game_base = shard.game_index_base(rank, games_per_rank)
     runner = SelfPlayRunner(net, sm, transformer, selfplay_conf(args.mode, evals), device=device,

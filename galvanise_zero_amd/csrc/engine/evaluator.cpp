@@ -135,12 +135,17 @@ PuctNode* PuctEvaluator::expandChild(PuctNode* parent, PuctNodeChild* child) {
     if (child->to_node != nullptr) {
         child->to_node->ref_count++;
         stats.num_transpositions_attached++;
+        mirror_ok = false;   // a node with two parents: only one of them holds its mirror
     } else {
         child->unselectable = true;
         parent->unselectable_count++;
+        parent->syncParent();
         child->to_node = createNode(parent, basestate_expand_node.data());
         parent->unselectable_count--;
+        parent->syncParent();
         child->unselectable = false;
+        child->to_node->in_parent = child;
+        child->to_node->syncParent();
     }
     return child->to_node;
 }
@@ -249,6 +254,13 @@ static inline bool visitsBefore(const PuctNodeChild* a, const PuctNodeChild* b) 
     if (va == vb) return a->policy_prob > b->policy_prob;
     return va > vb;
 }
+// the same from the children's mirrors (node.h)
+static inline bool visitsBeforeM(const PuctNodeChild* a, const PuctNodeChild* b) {
+    const int va = a->to_node == nullptr ? 0 : (int)a->m_visits;
+    const int vb = b->to_node == nullptr ? 0 : (int)b->m_visits;
+    if (va == vb) return a->policy_prob > b->policy_prob;
+    return va > vb;
+}
 
 // chooseTopVisits (evaluator.cpp:1100-1136) as one unsorted pass: first win, first two non-losses
 // and first overall under travBefore, with tie flags.  add() per child, then finish().
@@ -258,9 +270,13 @@ struct TopVisitsScan {
     int a_n = 0, b_n = 0;
 
     __attribute__((always_inline)) inline void add(const PuctNodeChild* c, int ri) {
+        const bool fin = c->to_node != nullptr && c->to_node->is_finalised;
+        addMirrored(c, fin, fin ? c->to_node->getCurrentScore(ri) : 0.0f);
+    }
+    // the same with the child node's is_finalised / current score (of role ri) supplied
+    __attribute__((always_inline)) inline void addMirrored(const PuctNodeChild* c, bool fin, Score sc) {
         bool win = false, loss = false;
-        if (c->to_node != nullptr && c->to_node->is_finalised) {
-            const Score sc = c->to_node->getCurrentScore(ri);
+        if (fin) {
             win = sc > 0.99;
             loss = !win && sc < 0.01;
         }
@@ -340,22 +356,23 @@ bool PuctEvaluator::convergedFast(int count, bool* out) const {
     const PuctNodeChild* cs = root->children();
     const PuctNodeChild *a = nullptr, *b = nullptr;
     int a_n = 0, b_n = 0;
+    auto before = mirror_ok ? visitsBeforeM : visitsBefore;
     for (int i = 0; i < n; ++i) {
         const PuctNodeChild* c = cs + i;
         if (a == nullptr) {
             a = c;
             a_n = 1;
-        } else if (visitsBefore(c, a)) {
+        } else if (before(c, a)) {
             b = a;
             b_n = a_n;
             a = c;
             a_n = 1;
-        } else if (!visitsBefore(a, c)) {
+        } else if (!before(a, c)) {
             a_n++;
-        } else if (b == nullptr || visitsBefore(c, b)) {
+        } else if (b == nullptr || before(c, b)) {
             b = c;
             b_n = 1;
-        } else if (!visitsBefore(b, c)) {
+        } else if (!before(b, c)) {
             b_n++;
         }
     }
@@ -578,32 +595,54 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
     bool win_tied = false, rng_steps = false;
     float win_key = 0.f;
     int latch_d = -1, latch_count = 0, reach = 0;
+    const bool M = mirror_ok;   // read the children's mirrors (node.h) instead of their nodes
     for (int i = 0; i < n; ++i) {
         PuctNodeChild* c = cs + i;
         const PuctNode* cn = c->to_node;
-        if (want_top) top.add(c, lead);
-        if (cn != nullptr && cn->visits > 0) total_policy_visited += c->policy_prob;
-        S.key_s[i] = cn == nullptr ? -1 : cn->getCurrentScore(lead);
+        // the child node's fields this pass reads
+        uint32_t cn_visits = 0;
+        float cn_score = -1;
+        uint16_t cn_inflight = 0;
+        uint8_t cn_flags = 0;
+        if (cn != nullptr) {
+            if (M) {
+                cn_visits = c->m_visits;
+                cn_score = c->m_score;
+                cn_inflight = c->m_inflight;
+                cn_flags = c->m_flags;
+            } else {
+                cn_visits = cn->visits;
+                cn_score = cn->getCurrentScore(lead);
+                cn_inflight = cn->inflight_visits;
+                cn_flags = (uint8_t)((cn->is_finalised ? kMirrorFinalised : 0) |
+                                     (cn->num_children > 0 && cn->unselectable_count == cn->num_children
+                                          ? kMirrorAllUnselectable : 0));
+            }
+        }
+        const bool cn_final = (cn_flags & kMirrorFinalised) != 0;
+        if (want_top) top.addMirrored(c, cn != nullptr && cn_final, cn_score);
+        if (cn != nullptr && cn_visits > 0) total_policy_visited += c->policy_prob;
+        S.key_s[i] = cn == nullptr ? -1 : cn_score;
         S.key_p[i] = c->policy_prob_orig;
 
         S.kind[i] = kSkip;
         if (c->unselectable) continue;
-        if (cn != nullptr && cn->num_children > 0 && cn->unselectable_count == cn->num_children) continue;
+        if (cn != nullptr && (cn_flags & kMirrorAllUnselectable)) continue;
         const int traversals = c->traversals + 1;
-        const double inflight_visits = cn != nullptr ? cn->inflight_visits : 0;
+        const double inflight_visits = cn != nullptr ? cn_inflight : 0;
         double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
                                    (traversals + inflight_visits);
         S.trav[i] = c->traversals;
         S.inflight[i] = inflight_visits;
         if (c->traversals > 0 && inflight_visits > 0) rng_steps = true;   // discount draws RNG
         if (cn != nullptr) {
-            double child_score = cn->getCurrentScore(lead);
-            if (cn->is_finalised) {
+            double child_score = cn_score;
+            if (cn_final) {
                 if (child_score > 0.99) {
                     if (depth > 0) {
                         // the first win in sortedChildrenSelect order has the highest current score
                         S.kind[i] = kWinReturn;
-                        const float k = cn->getCurrentScore(lead);
+                        const float k = cn_score;
                         if (win < 0 || k > win_key) {
                             win = i;
                             win_key = k;
@@ -623,7 +662,7 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
             }
             S.kind[i] = kScored;
             S.base[i] = child_score;
-            S.bcs[i] = cn->is_finalised || cn->visits > 42;
+            S.bcs[i] = cn_final || cn_visits > 42;
         } else {
             S.kind[i] = kPrior;
         }
@@ -889,6 +928,7 @@ void PuctEvaluator::backup(float* new_scores, const Path& path) {
 
         cur.node->visits++;
         if (cur.node->inflight_visits > 0) cur.node->inflight_visits--;
+        cur.node->syncParent();
 
         if (cur.choice != nullptr) {
             cur.choice->traversals++;
@@ -944,6 +984,7 @@ int PuctEvaluator::treePlayout(PuctNode* current, Path& path) {
             }
         }
         current->inflight_visits++;
+        current->syncParent();
         current = child->to_node;
     }
 
@@ -959,27 +1000,30 @@ int PuctEvaluator::treePlayout(PuctNode* current, Path& path) {
 // With two or more finalised winning children at the root, the reference's playout loop is never
 // "converged" (the two most visited children are wins with equal scores) and runs until enough NN
 // evaluations accumulate -- up to millions of playouts per move, nearly all of them root -> win ->
-// backup with no evaluation (playoutMain, evaluator.cpp:744-886).  While the other candidates
-// provably cannot be selected, such a playout only needs the winning children's scores: spinPlayout
-// runs one playout of that form with the reference's arithmetic and RNG consumption (the root-latch
-// draw per reaching child), and returns false whenever the proof does not hold, after which the
-// ordinary treePlayout runs.
+// backup with no evaluation (playoutMain, evaluator.cpp:744-886).  Such a playout only needs the
+// scores of the few children that can still win the selection: spinPlayout runs one playout of
+// that form with the reference's arithmetic and RNG consumption (the root-latch draw per reaching
+// child), and returns false whenever the proof below does not hold or another child wins the
+// selection, after which the ordinary treePlayout runs.
 //
 // An epoch (spinBuild, one pass over the children) establishes, for root visits v in [v0, v_end):
 //   * no child is in flight, none is unselectable or being expanded, the Dirichlet noise cannot
-//     change, backup_finalised is off (the root cannot become finalised);
-//   * every non-win candidate i scores at most U_i = base_i + (float)(pc(v_end-1) * p_i) *
+//     change, backup_finalised is off (the root cannot become finalised), no child can reach the
+//     root-latch threshold except the wins (checked per playout);
+//   * every other candidate i scores at most U_i = base_i + (float)(pc(v_end-1) * p_i) *
 //     sqrt(v_end) / (t_i + 1), the value its exploration term reaches at the epoch's last playout
-//     (pc and sqrt increase with v, its traversals and policy_prob do not change inside the epoch:
-//     it is never selected and normaliseX -- every 100 root visits -- ends the epoch), with base_i =
-//     its current score, or for unexpanded children the FPU prior, bounded by the top win's score;
-//   * the best win scores at least min_w s_w * (1 + pc(v0)) > max_i U_i (with a relative margin
-//     covering the float truncations of the selection's comparisons);
+//     (pc and sqrt increase with v; its traversals and policy_prob do not change while it is not
+//     selected, and normaliseX -- every 100 root visits -- ends the epoch), with base_i its current
+//     score, or for unexpanded children the FPU prior, bounded by the top win's score;
+//   * candidates whose bound reaches the wins' floor min_w s_w * (1 + pc(v0)) are WATCHED: scored
+//     exactly every playout (an unexpanded one with the exact FPU prior, whose policy sum is folded
+//     over the visited children in index order as the reference does);
 //   * the two most visited children are wins with equal scores, so converged() is false for the
-//     whole epoch (only wins gain visits), and no non-win can reach the root latch threshold.
-// Per playout only the winning children are scored, in the order sortedChildrenSelect gives them
-// (constant inside the epoch: no sort key changes), with the reference loop's `score > best_score`
-// (float) semantics: exact ties between wins resolve as in the reference.
+//     whole epoch (only wins gain visits) -- or playoutMain evaluates it as usual.
+// Per playout the wins and watched candidates are scored in sortedChildrenSelect order (constant in
+// the epoch: no sort key changes) with the reference loop's `score > best_score` (float) semantics;
+// the result stands when it is a win and beats every unwatched bound with margin (unwatched
+// elements below the final best cannot change the loop's outcome).
 
 static bool spin_fast_enabled() {
     static const bool v = [] {
@@ -988,6 +1032,9 @@ static bool spin_fast_enabled() {
     }();
     return v;
 }
+
+static inline double spin_margin_up(double x) { return x + std::fabs(x) * 1e-6 + 1e-12; }
+static inline double spin_margin_down(double x) { return x - std::fabs(x) * 1e-6 - 1e-12; }
 
 bool PuctEvaluator::spinBuild() {
     spin.valid = false;
@@ -1003,7 +1050,7 @@ bool PuctEvaluator::spinBuild() {
     const uint32_t v0 = node->visits;
     PuctNodeChild* cs = node->children();
     const int n = node->num_children;
-    int nw = 0, reach = 0;
+    int nw = 0, reach = 0, nvis = 0;
     float win_score = 0.f;
     uint32_t wv0 = 0, wv1 = 0;   // the two largest win visit counts
     uint32_t nonwin_max_visits = 0;
@@ -1013,15 +1060,19 @@ bool PuctEvaluator::spinBuild() {
         const PuctNode* cn = c->to_node;
         if (c->unselectable) return false;
         if (cn != nullptr) {
+            if (cn->visits > 0) {
+                if (nvis == SpinEpoch::kMaxVisited) return false;
+                spin.visited[nvis++] = (uint16_t)i;
+            }
             if (cn->inflight_visits != 0) return false;
             if (cn->num_children > 0 && cn->unselectable_count == cn->num_children) return false;
             if (cn->is_finalised) {
                 const float sc = cn->getCurrentScore(lead);
                 if (sc > 0.99) {
-                    if (!cn->isTerminal() || nw == 8) return false;
+                    if (!cn->isTerminal() || nw == SpinEpoch::kMaxWins) return false;
                     if (nw > 0 && !(sc == win_score)) return false;
                     win_score = sc;
-                    spin.wins[nw++] = (uint16_t)i;
+                    ++nw;
                     if (cn->visits >= wv0) { wv1 = wv0; wv0 = cn->visits; }
                     else if (cn->visits > wv1) wv1 = cn->visits;
                     ++reach;
@@ -1055,15 +1106,18 @@ bool PuctEvaluator::spinBuild() {
     // the best win scores at least its child_score = s_w * (1 + pc(v)) >= s_w * (1 + pc(v0))
     double floor_win = win_score;
     floor_win *= 1.0f + pc_at(v0);
-    const double floor_adj = floor_win - std::fabs(floor_win) * 1e-6 - 1e-12;
+    const double floor_adj = spin_margin_down(floor_win);
 
     uint32_t v_end = (v0 / 100 + 1) * 100;   // normaliseX at the backup reaching a multiple of 100
     for (int attempt = 0; attempt < 4; ++attempt) {
         const uint32_t vl = v_end - 1;         // the epoch's last selection
         const float pc = pc_at(vl);
         const double sq = std::sqrt(vl + 1);
-        double bound = -1e300;
-        for (int i = 0; i < n; ++i) {
+        double unwatched = -1e300;
+        int nwatch = 0;
+        bool watch_prior = false;
+        bool ok = true;
+        for (int i = 0; i < n && ok; ++i) {
             const PuctNodeChild* c = cs + i;
             const PuctNode* cn = c->to_node;
             double base, expl;
@@ -1076,12 +1130,20 @@ bool PuctEvaluator::spinBuild() {
                 base = sc;
                 expl = cn->is_finalised ? 0.0 : pc * c->policy_prob * sq / (c->traversals + 1 + 0.0);
             }
-            bound = std::max(bound, base + expl);
+            const double u = spin_margin_up(base + expl);
+            if (u < floor_adj) {
+                unwatched = std::max(unwatched, u);
+            } else if (nwatch == SpinEpoch::kMaxWatched) {
+                ok = false;
+            } else {
+                spin.watched_flag[nwatch++] = (uint16_t)i;   // temporarily: indices
+                watch_prior = watch_prior || cn == nullptr;
+            }
         }
-        const double bound_adj = bound + std::fabs(bound) * 1e-6 + 1e-12;
-        if (bound_adj < floor_adj) {
-            // the wins in sortedChildrenSelect order (evaluator.cpp:242-263; equal-score wins are
-            // equivalent under its comparator, so std::sort's permutation decides)
+        if (ok) {
+            // wins and watched candidates in sortedChildrenSelect order (evaluator.cpp:242-263;
+            // equal-score wins are equivalent under its comparator, so std::sort's permutation
+            // decides)
             SelectScratch& S = t_sel;
             S.reserve(n);
             for (int i = 0; i < n; ++i) {
@@ -1090,18 +1152,35 @@ bool PuctEvaluator::spinBuild() {
                 S.key_p[i] = cs[i].policy_prob_orig;
             }
             const uint16_t* order = S.sortedOrder(n);
-            int k = 0;
+            int k = 0, kw = 0;
             for (int j = 0; j < n; ++j) {
-                const PuctNode* cn = cs[order[j]].to_node;
-                if (cn != nullptr && cn->is_finalised && cn->getCurrentScore(lead) > 0.99) spin.wins[k++] = order[j];
+                const int i = order[j];
+                const PuctNode* cn = cs[i].to_node;
+                if (cn != nullptr && cn->is_finalised && cn->getCurrentScore(lead) > 0.99) {
+                    spin.cand[k] = (uint16_t)i;
+                    spin.cand_kind[k++] = SpinEpoch::kWin;
+                    ++kw;
+                    continue;
+                }
+                for (int w = 0; w < nwatch; ++w)
+                    if (spin.watched_flag[w] == i) {
+                        spin.cand[k] = (uint16_t)i;
+                        spin.cand_kind[k++] = cn == nullptr ? SpinEpoch::kPrior : SpinEpoch::kScored;
+                        break;
+                    }
             }
-            if (k != nw) return false;
+            // (a comparator that is not a strict weak ordering -- the reference's, with negative
+            // scores next to unexpanded children -- may drop or repeat elements: ordinary path)
+            if (kw != nw || k != nw + nwatch) return false;
+            spin.ncand = k;
+            spin.nvisited = nvis;
+            spin.watch_prior = watch_prior;
+            spin.win_score = win_score;
+            spin.unwatched_bound = unwatched;
             spin.conv_false = conv_false;
             spin.root = node;
             spin.v_end = v_end;
             spin.reach = reach;
-            spin.nwins = nw;
-            spin.nonwin_bound = bound_adj;
             spin.valid = true;
             return true;
         }
@@ -1130,39 +1209,60 @@ bool PuctEvaluator::spinPlayout() {
         return false;
     }
 
-    // selectChild (evaluator.cpp:341-517) restricted to the winning children
+    // selectChild (evaluator.cpp:341-517) restricted to the wins and the watched candidates
     setPuctConstant(node, 0);
     const double sqrt_node_visits = std::sqrt(node->visits + 1);
     PuctNodeChild* cs = node->children();
-    float best_score = -1;
-    int best = -1;
-    double min_score = 1e300;
     const bool latch = node->visits > 1000 && node->visits < 40000000;
     const float limit_latch_root = 0.66;
-    for (int k = 0; k < spin.nwins; ++k) {
-        const int i = spin.wins[k];
+    float prior_score = 0.f;
+    if (spin.watch_prior) {
+        // priorScore (evaluator.cpp:1195-1224): the top-visits child is a win; the policy sum of
+        // the visited children accumulates in child order
+        float total_policy_visited = 0.0;
+        for (int k = 0; k < spin.nvisited; ++k) total_policy_visited += cs[spin.visited[k]].policy_prob;
+        prior_score = spin.win_score;
+        float fpu_reduction = conf->fpu_prior_discount_root;
+        if (fpu_reduction > 0) {
+            fpu_reduction *= std::sqrt(total_policy_visited);
+            prior_score -= fpu_reduction;
+        }
+    }
+    float best_score = -1;
+    int best = -1;
+    bool best_win = false;
+    double best_exact = 0.0;
+    for (int k = 0; k < spin.ncand; ++k) {
+        const int i = spin.cand[k];
+        const uint8_t kind = spin.cand_kind[k];
         PuctNodeChild* c = cs + i;
         const PuctNode* cn = c->to_node;
-        if (latch && c->traversals > 16 && c->traversals > node->visits * limit_latch_root) {
+        if (kind == SpinEpoch::kWin && latch && c->traversals > 16 &&
+            c->traversals > node->visits * limit_latch_root) {
             spin.valid = false;
             return false;
         }
         const int traversals = c->traversals + 1;
-        const double inflight_visits = cn->inflight_visits;
-        const double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
-                                         (traversals + inflight_visits);
-        double child_score = cn->getCurrentScore(lead);
-        child_score *= 1.0f + node->puct_constant;
+        const double inflight_visits = cn != nullptr ? cn->inflight_visits : 0;
+        double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
+                                   (traversals + inflight_visits);
+        double child_score = prior_score;
+        if (cn != nullptr) {
+            child_score = cn->getCurrentScore(lead);
+            if (kind == SpinEpoch::kWin) child_score *= 1.0f + node->puct_constant;
+            else if (cn->is_finalised) exploration_score = 0.0;
+        }
         const double score = child_score + exploration_score;
-        min_score = std::min(min_score, score);
         if (score > best_score) {   // the reference loop (evaluator.cpp:487-490), float best_score
             best = i;
             best_score = score;
+            best_win = kind == SpinEpoch::kWin;
+            best_exact = score;
         }
     }
-    // every win outscores every other candidate (the epoch bound), so the loop over all children
-    // in sorted order ends on the same child as this loop over the wins
-    if (!(spin.nonwin_bound < min_score) || !(spin.nonwin_bound <= (double)(float)min_score)) {
+    // a watched candidate wins (its playout descends: ordinary path), or the result is not
+    // separated from the unwatched bound
+    if (!best_win || !(spin.unwatched_bound < best_exact) || !(spin.unwatched_bound <= (double)(float)best_exact)) {
         spin.valid = false;
         return false;
     }
@@ -1194,6 +1294,7 @@ bool PuctEvaluator::spinPlayout() {
     path.clear();
     path.emplace_back(node, chosen, chosen);
     node->inflight_visits++;
+    node->syncParent();
     path.emplace_back(leaf, nullptr, nullptr);
     stats.playouts_finals++;
     float scores[kMaxRoles];
@@ -1303,6 +1404,7 @@ PuctNode* PuctEvaluator::fastApplyMove(const PuctNodeChild* next) {
 
     GZ_ASSERT(new_root != nullptr);
     root = new_root;
+    root->in_parent = nullptr;   // a root's mirror is never read
     game_depth++;
     return root;
 }
@@ -1330,6 +1432,7 @@ void PuctEvaluator::reset(int depth) {
     }
     stats.reset();
     game_depth = depth;
+    mirror_ok = true;
 }
 
 // evaluator.cpp:1006-1017

@@ -101,13 +101,21 @@ private:
     // Root spin fast path (evaluator.cpp, "spin"): playouts that go root -> finalised winning
     // child, run without the full selection pass while provably nothing else can be chosen.
     struct SpinEpoch {
+        static constexpr int kMaxWins = 8, kMaxWatched = 6, kMaxVisited = 96;
+        enum : uint8_t { kWin = 0, kScored = 1, kPrior = 2 };
         const PuctNode* root = nullptr;
         uint32_t v_end = 0;          // the epoch holds while root->visits < v_end
         uint32_t retry_at = 0;       // after a failed build: next attempt at this root visit count
         int reach = 0;               // selection candidates (root-latch RNG draws per playout)
-        int nwins = 0;
-        uint16_t wins[8];            // root children that are finalised wins, in sortedChildrenSelect order
-        double nonwin_bound = 0;     // upper bound of every other candidate's score until v_end
+        int ncand = 0;               // wins + watched candidates, in sortedChildrenSelect order
+        uint16_t cand[kMaxWins + kMaxWatched];
+        uint8_t cand_kind[kMaxWins + kMaxWatched];
+        uint16_t watched_flag[kMaxWatched];
+        int nvisited = 0;            // children with visits > 0, in child order (FPU policy sum)
+        uint16_t visited[kMaxVisited];
+        bool watch_prior = false;    // an unexpanded child is watched: the exact FPU prior is needed
+        float win_score = 0.f;
+        double unwatched_bound = 0;  // upper bound of every unwatched candidate's score until v_end
         bool conv_false = false;     // converged() proved false for the epoch
         bool valid = false;
     };
@@ -143,6 +151,7 @@ private:
     long total_evaluations = 0;
     long total_tree_playouts = 0;   // diagnostics: NN-free playouts = tree playouts - evaluations
     bool do_playouts = false;
+    bool mirror_ok = true;   // every node has one parent: the child mirrors (node.h) are exact
     PlayoutStats stats;
     Rng rng;
 };

@@ -29,6 +29,10 @@ static int initialiseChildHelper(PuctNode* node, int role_index, int child_index
             child->to_node = nullptr;
             child->unselectable = false;
             child->use_minimax = false;
+            child->m_flags = 0;
+            child->m_score = 0.0f;
+            child->m_visits = 0;
+            child->m_inflight = 0;
             child->traversals = 0;
             child->policy_prob_orig = 1.0f;
             child->policy_prob = 1.0f;
@@ -75,6 +79,7 @@ PuctNode* PuctNode::create(const uint64_t* base_state, StateMachine* sm) {
     const size_t bytes = node_bytes(total_children, role_count, num_words);
     PuctNode* node = static_cast<PuctNode*>(std::aligned_alloc(64, bytes));
     node->parent = nullptr;
+    node->in_parent = nullptr;
     node->visits = 0;
     node->inflight_visits = 0;
     node->ref_count = 1;

@@ -20,6 +20,7 @@ struct PuctNodeChild {
     PuctNode* to_node;
     bool unselectable;
     bool use_minimax;
+    uint8_t m_flags;         // mirror: kMirrorFinalised | kMirrorAllUnselectable
     uint32_t traversals;
     float policy_prob_orig;
     float policy_prob;
@@ -27,7 +28,16 @@ struct PuctNodeChild {
     Score debug_node_score;
     Score debug_puct_score;
     JointMove move;
+    // Mirror of the fields of to_node a selection pass over the parent reads (build layout, not in
+    // the reference): kept current by PuctNode::syncParent() at every change of to_node, so the
+    // selection streams the parent's child array instead of dereferencing one node per child.
+    // Valid while to_node != nullptr.
+    Score m_score;           // to_node's current score for the parent's lead role
+    uint32_t m_visits;
+    uint16_t m_inflight;
 };
+
+constexpr uint8_t kMirrorFinalised = 1, kMirrorAllUnselectable = 2;
 
 typedef std::vector<const PuctNodeChild*> Children;
 
@@ -35,25 +45,39 @@ struct PuctNode {
     static constexpr int lead_role_index_simultaneous = -1;
 
     const PuctNode* parent;
+    PuctNodeChild* in_parent;   // the parent's child entry mirroring this node (null for a root)
+    // Current scores live in the header: together with visits / is_finalised / unselectable_count
+    // they are what the parent's mirror copies; the header is one 64-byte line (nodes are 64-byte
+    // aligned).
+    Score current[kMaxRoles];
     uint32_t visits;
+    float puct_constant;
+    uint32_t allocated_size;
     uint16_t inflight_visits;
     uint16_t ref_count;
     uint16_t unselectable_count;
     uint16_t num_children;
     uint16_t num_children_expanded;
-    float puct_constant;
+    int16_t lead_role_index;
+    uint16_t game_depth;
+    uint16_t num_words;
     bool is_finalised;
     bool force_terminal;
     bool dirichlet_noise_set;
-    int16_t lead_role_index;
-    uint16_t game_depth;
     uint8_t role_count;
-    uint16_t num_words;
-    uint32_t allocated_size;
-    // Current scores live in the header: together with visits / is_finalised / unselectable_count
-    // they are all a parent's selection passes read of a child node, and the header is one 64-byte
-    // line (nodes are 64-byte aligned), so each child costs one cache line, not two.
-    Score current[kMaxRoles];
+
+    // refresh the parent's mirror entry after a change of visits / current / inflight_visits /
+    // is_finalised / unselectable_count
+    void syncParent() {
+        PuctNodeChild* e = in_parent;
+        if (e == nullptr) return;
+        const int lead = parent->lead_role_index < 0 ? 0 : parent->lead_role_index;
+        e->m_score = current[lead];
+        e->m_visits = visits;
+        e->m_inflight = inflight_visits;
+        e->m_flags = (uint8_t)((is_finalised ? kMirrorFinalised : 0) |
+                               (num_children > 0 && unselectable_count == num_children ? kMirrorAllUnselectable : 0));
+    }
 
     // trailing storage: children[num_children] | final[R] | basestate words
     PuctNodeChild* children() { return reinterpret_cast<PuctNodeChild*>(this + 1); }

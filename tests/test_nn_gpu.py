@@ -1,8 +1,9 @@
 """GPU parity of the fused HIP forward (libgz_nn.so via its C-ABI) against the oracle.
 
 Stated tolerance (bf16 MFMA operands, fp32 accumulate, fp32 residual stream and heads), measured
-against the float64 reference semantics oracle/nn_ref.forward:
-    policies / values: max |err| <= 5e-2, mean |err| <= 5e-3     (TOL_REF)
+against the float64 reference semantics oracle/nn_ref.forward: per variant, 3x the max / mean abs
+error measured on MI355X for these seeded inputs (profiles/r02c_gpu_tests.log), TOL_BF16 below.
+The fp32-accuracy mode (split hi/lo operands) has its own, ~100x tighter tolerance (TOL_FP32).
 and against the bf16-emulating oracle (same rounding points as the kernel, differing only in
 accumulation order, which flips an occasional bf16 rounding of an activation; the flips compound
 with depth):
@@ -21,7 +22,12 @@ from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS, NetDesc
 from galvanise_zero_amd.nn.weights import random_planes, random_weights, to_blob
 from oracle import nn_ref
 
-TOL_REF = (5e-2, 5e-3)
+# 3 x measured (max, mean) abs error vs the float64 oracle, bf16 mode (profiles/r02c_gpu_tests.log)
+TOL_BF16 = {"cfg1": (6.4e-3, 1.4e-4), "cfg2": (7.5e-2, 9.3e-3), "b0_8x8": (2.6e-3, 1.6e-3),
+            "leaky_v3_8x8": (1e-2, 9e-4), "nchw_6x6": (3.3e-3, 1e-3), "cfg3": (3.2e-3, 1e-3),
+            "cfg4": (7e-4, 2.5e-5), "cfg5": (3.1e-3, 1.4e-3), "b2_13x13_f256": (1.3e-2, 2.4e-3),
+            "b0_10x10_f256_v3": (1e-3, 4.1e-4), "legacy_v1_8x8": (8.7e-3, 1.1e-4), "x6_102_json": (5e-4, 2.5e-4)}
+TOL_REF = TOL_BF16["cfg2"]
 TOL_EMU_SHALLOW = (2e-3, 2e-5)
 TOL_EMU_DEEP = (2e-2, 5e-3)
 
@@ -81,7 +87,8 @@ def test_forward_parity(name, hip_device):
             er, ee = _err(g, r), _err(g, e)
             print("%s n=%d out%d  vs_ref max %.3g mean %.3g | vs_emu max %.3g mean %.3g"
                   % (name, n, i, er[0], er[1], ee[0], ee[1]))
-            assert er[0] <= TOL_REF[0] and er[1] <= TOL_REF[1], (name, n, i, er)
+            tol = TOL_BF16[name]
+            assert er[0] <= tol[0] and er[1] <= tol[1], (name, n, i, er)
             assert ee[0] <= tol_emu[0] and ee[1] <= tol_emu[1], (name, n, i, ee)
             if not (desc.value_sigmoid and i == len(got) - 1):   # sigmoid values are independent
                 np.testing.assert_allclose(g.sum(axis=1), 1.0, atol=1e-4)
@@ -134,8 +141,9 @@ def test_kernel_variants_identical(variant, hip_device, monkeypatch):
 # ---- fp32-accuracy mode (split hi/lo bf16 operands, three MFMAs per product) ------------------
 # Stated tolerance against the float64 oracle (reference semantics), per output element and per
 # row (KL divergence of each policy / value row from the oracle's):
-TOL_FP32 = (1e-3, 1e-5)          # max |err|, mean |err| -- set from the measured errors
-TOL_FP32_KL = 1e-6               # max over rows of KL(oracle || kernel)
+# 3 x the worst measured over SPLIT (max 6.7e-5, mean 1.6e-5, KL 1.4e-7; profiles/r02c_gpu_tests.log)
+TOL_FP32 = (2e-4, 5e-5)          # max |err|, mean |err|
+TOL_FP32_KL = 5e-7               # max over rows of KL(oracle || kernel)
 SPLIT = ["cfg1", "cfg2", "cfg3", "b0_8x8", "leaky_v3_8x8", "nchw_6x6", "legacy_v1_8x8", "x6_102_json"]
 
 
