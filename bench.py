@@ -44,8 +44,8 @@ NUM_CUS = 256
 # PMC-measured fabric bytes per trunk launch (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE,
 # separate rocprofv3 --pmc passes, tools/gpu_pmc.sh).  PMC counters cannot be read inside the timed
 # run, so the figure measured for the same kernel is reported with its source.
-TRAFFIC_PER_LAUNCH = {"gznn::trunk_kernel<128, 8, 8, 1, 1>": (14290.1 * 2 + 320.0) * 1024,
-                      "gznn::trunk_kernel<128, 8, 8, 2, 1>": (14722.3 * 2 + 800.0) * 1024}
+TRAFFIC_PER_LAUNCH = {"gznn::trunk_kernel<128, 8, 8, 1, 1, 1>": (14290.1 * 2 + 320.0) * 1024,
+                      "gznn::trunk_kernel<128, 8, 8, 2, 1, 1>": (14722.3 * 2 + 800.0) * 1024}
 TRAFFIC_SOURCE = "profiles/r01k_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 256- and 640-row launches)"
 
 
@@ -66,6 +66,10 @@ def parse():
                     help="BASELINE.json configs[i-1]; 2 (breakthrough 8x8, 6x128) is the headline workload, "
                          "3-5 (reversi 10x128, hexLG13 12x256, amazons_10x10 20x256) run the same path")
     ap.add_argument("--mode", choices=["template", "literal"], default="template")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
+                    help="trunk arithmetic: fp32 = split hi/lo bf16 operands, three MFMAs per product "
+                         "(fp32-class accuracy, the reference runs fp32 TF; default where the kernel "
+                         "has it, F <= 128); bf16 = bf16 operands (default for the F = 256 configs)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
@@ -249,7 +253,9 @@ def main():
     from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS
     evals = args.evals or BASELINE_CONFIGS[args.config]["evals"]
     sm, transformer, desc = setup_game(args.config)
-    net = HipNet(desc, device)
+    if args.precision is None:
+        args.precision = "fp32" if desc.cnn_filter_size <= 128 else "bf16"
+    net = HipNet(desc, device, args.precision)
 
     # weights: rank 0 creates, RCCL broadcast of the blob (the only collective on the path)
     blob = torch.empty(net.weight_count, dtype=torch.float32, device="cuda")
@@ -334,9 +340,10 @@ def main():
         # the trunk kernel runs as one of two variants by launch size; the roofline is reported for
         # the variant that took more trunk time, the other one alongside
         geo = (desc.cnn_filter_size, desc.input_columns, desc.input_rows)
+        p = 3 if args.precision == "fp32" else 1
         variants = {
-            "gznn::trunk_kernel<%d, %d, %d, 2, 1>" % geo: (l_launches, l_rows, l_tms),
-            "gznn::trunk_kernel<%d, %d, %d, 1, 1>" % geo: (launches - l_launches, rows - l_rows, tms - l_tms),
+            "gznn::trunk_kernel<%d, %d, %d, 2, 1, %d>" % (geo + (p,)): (l_launches, l_rows, l_tms),
+            "gznn::trunk_kernel<%d, %d, %d, 1, 1, %d>" % (geo + (p,)): (launches - l_launches, rows - l_rows, tms - l_tms),
         }
         per_variant = {}
         for name, (vl, vr, vt) in variants.items():
@@ -344,10 +351,14 @@ def main():
                 per_variant[name] = {"launches": vl, "rows_per_launch": vr / vl, "avg_kernel_ms": vt / vl,
                                      "achieved_tflops": desc.flops_trunk() * vr / (vt / 1e3) / 1e12}
         dom = max(per_variant, key=lambda k: variants[k][2]) if per_variant else None
-        # weight stream per trunk workgroup: bf16 3x3 conv weights of every residual conv
-        wbytes = 2 * desc.residual_layers * 9 * desc.cnn_filter_size ** 2 * 2
+        # weight stream per trunk workgroup: bf16 3x3 conv weights of every residual conv (hi + lo
+        # parts in fp32 mode)
+        wbytes = 2 * desc.residual_layers * 9 * desc.cnn_filter_size ** 2 * 2 * (2 if p == 3 else 1)
+        # the fp32-accuracy trunk issues 3 bf16 MFMAs per algorithmic product: its ceiling on
+        # algorithmic FLOP/s is a third of the dense bf16 peak
+        peak = PEAK_BF16_TFLOPS / p
         for name, pv in per_variant.items():
-            nb = 2 if name.endswith("2, 1>") else 1
+            nb = 2 if ", 2, 1, " in name else 1
             wg = pv["rows_per_launch"] / nb
             cus = min(wg, NUM_CUS)
             rate = wg * wbytes / (pv["avg_kernel_ms"] / 1e3) / cus / 1e9
@@ -377,7 +388,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp32 (split bf16 hi+lo operands, 3 MFMAs per product, fp32 accumulate)" if p == 3 else "bf16",
             "data": "synthetic: self-play from the initial position, random-init weights (no .h5 in reference)",
             "config": {"workload": "%s self-play (BASELINE configs[%d]), v1 %dx%d net, %d evals/move (%s mode), "
                                    "eval batch %d" % (sm.game, args.config - 1, desc.residual_layers,
@@ -390,8 +401,9 @@ def main():
                        "game_ranges": {"per_rank": ranges, "disjoint": disjoint},
                        "weights_broadcast": {"collective": "RCCL broadcast" if world > 1 else "none (1 rank)",
                                              "identical_on_all_ranks": abs(blob_sums - world * blob_sum) <= 1e-6 * max(1.0, abs(world * blob_sum))}},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_BF16_TFLOPS,
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak,
+                         "peak_basis": "dense bf16 MFMA %.0f TFLOP/s / %d MFMAs per algorithmic product" % (PEAK_BF16_TFLOPS, p),
                          "traffic": TRAFFIC_PER_LAUNCH.get(dom) if args.config == 2 else None,
                          "traffic_unit": "bytes/launch",
                          "traffic_source": TRAFFIC_SOURCE if args.config == 2 and dom in TRAFFIC_PER_LAUNCH else None,
