@@ -44,8 +44,8 @@ NUM_CUS = 256
 # PMC-measured fabric bytes per trunk launch (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE,
 # separate rocprofv3 --pmc passes, tools/gpu_pmc.sh).  PMC counters cannot be read inside the timed
 # run, so the figure measured for the same kernel is reported with its source.
-TRAFFIC_PER_LAUNCH = {"gznn::trunk_kernel<128, 8, 8, 1, 1, 1>": (14290.1 * 2 + 320.0) * 1024,
-                      "gznn::trunk_kernel<128, 8, 8, 2, 1, 1>": (14722.3 * 2 + 800.0) * 1024}
+TRAFFIC_PER_LAUNCH = {"gznn::trunk_kernel<128, 4, 1, 1, 1>": (14290.1 * 2 + 320.0) * 1024,
+                      "gznn::trunk_kernel<128, 4, 2, 1, 1>": (14722.3 * 2 + 800.0) * 1024}
 TRAFFIC_SOURCE = "profiles/r01k_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 256- and 640-row launches)"
 
 
@@ -339,17 +339,30 @@ def main():
         rows_per_launch = rows / launches if launches else float("nan")
         # the trunk kernel runs as one of two variants by launch size; the roofline is reported for
         # the variant that took more trunk time, the other one alongside
-        geo = (desc.cnn_filter_size, desc.input_columns, desc.input_rows)
+        # kernels are compiled per (padded filters, 16-position tiles): trunk_kernel<F, PT, NB, WPE, P>
+        fpad = 64 if desc.cnn_filter_size <= 64 else 128 if desc.cnn_filter_size <= 128 else 256
+        geo = (fpad, (desc.hw + 15) // 16)
         p = 3 if args.precision == "fp32" else 1
         variants = {
-            "gznn::trunk_kernel<%d, %d, %d, 2, 1, %d>" % (geo + (p,)): (l_launches, l_rows, l_tms),
-            "gznn::trunk_kernel<%d, %d, %d, 1, 1, %d>" % (geo + (p,)): (launches - l_launches, rows - l_rows, tms - l_tms),
+            "gznn::trunk_kernel<%d, %d, 2, 1, %d>" % (geo + (p,)): (l_launches, l_rows, l_tms),
+            "gznn::trunk_kernel<%d, %d, 1, 1, %d>" % (geo + (p,)): (launches - l_launches, rows - l_rows, tms - l_tms),
+        }
+        # the same over the whole run (aging included): what a rocprofv3 summary of this command
+        # averages over
+        whole = {
+            "gznn::trunk_kernel<%d, %d, 2, 1, %d>" % (geo + (p,)): (s1["large_launches"], s1["large_rows"], s1["large_trunk_ms"]),
+            "gznn::trunk_kernel<%d, %d, 1, 1, %d>" % (geo + (p,)): (s1["kernel_launches"] - s1["large_launches"],
+                                                                   s1["rows"] - s1["large_rows"],
+                                                                   s1["trunk_ms"] - s1["large_trunk_ms"]),
         }
         per_variant = {}
         for name, (vl, vr, vt) in variants.items():
             if vl > 0 and vt > 0:
+                wl, wr, wt = whole[name]
                 per_variant[name] = {"launches": vl, "rows_per_launch": vr / vl, "avg_kernel_ms": vt / vl,
-                                     "achieved_tflops": desc.flops_trunk() * vr / (vt / 1e3) / 1e12}
+                                     "achieved_tflops": desc.flops_trunk() * vr / (vt / 1e3) / 1e12,
+                                     "whole_run": {"launches": wl, "rows_per_launch": wr / max(wl, 1),
+                                                   "avg_kernel_ms": wt / max(wl, 1)}}
         dom = max(per_variant, key=lambda k: variants[k][2]) if per_variant else None
         # weight stream per trunk workgroup: bf16 3x3 conv weights of every residual conv (hi + lo
         # parts in fp32 mode)
@@ -358,7 +371,7 @@ def main():
         # algorithmic FLOP/s is a third of the dense bf16 peak
         peak = PEAK_BF16_TFLOPS / p
         for name, pv in per_variant.items():
-            nb = 2 if ", 2, 1, " in name else 1
+            nb = 2 if name.endswith(", 2, 1, %d>" % p) else 1
             wg = pv["rows_per_launch"] / nb
             cus = min(wg, NUM_CUS)
             rate = wg * wbytes / (pv["avg_kernel_ms"] / 1e3) / cus / 1e9

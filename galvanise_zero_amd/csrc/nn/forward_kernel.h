@@ -77,12 +77,20 @@ struct KParams {
     Segment seg[kMaxSegments];
     unsigned long long* stamps;   // diagnostics only (GZ_KERNEL_STAMPS): [grid][8] s_memtime per phase
     int C, K0, B, R, VH, V, leaky, flatten_nchw, maxP, npos;
+    int H, W, wmagic;        // board rows / columns; wmagic = ceil(65536 / W) (Board::div)
     int value_sigmoid;       // legacy model files: independent sigmoid per value output
     int btab_off;            // LDS byte offset of the trunk bias table
     int P[kMaxRoles];
 };
 
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
+
+// The board geometry at run time (kernels are compiled per filter count and position-tile count):
+// p / W as (p * ceil(65536 / W)) >> 16, exact for W <= 32 and p < 1024 (checked on the host).
+struct Board {
+    int H, W, npos, wmagic;
+    __device__ __forceinline__ int row(int p) const { return (p * wmagic) >> 16; }
+};
 
 // ring depth: largest R dividing the stages per conv with R slots of KS*CT fragments <= cap VGPRs
 __host__ __device__ constexpr int ring_depth(int nst, int ks, int ct, int cap) {
@@ -95,18 +103,24 @@ __host__ __device__ constexpr int ring_depth(int nst, int ks, int ct, int cap) {
 // P = 1: bf16 operands.  P = 3: split precision ("fp32 accuracy"): every fp32 operand x is carried
 // as x_hi = bf16(x), x_lo = bf16(x - x_hi) and each product as hi*hi + hi*lo + lo*hi (three MFMAs,
 // fp32 accumulation): ~16 significant bits per operand instead of 8.
-template <int F, int H, int W, int NB = 1, int P = 1>
+template <int F, int PTN, int NB = 1, int P = 1>
 struct Geo {
     static constexpr int P2 = P == 3 ? 2 : 1;        // bf16 parts per operand
-    static constexpr int NPOS = H * W;
-    static constexpr int PT = (NPOS + 15) / 16;      // position tiles per board (MFMA N)
+    // the board (H x W, runtime: kp.H / kp.W) has at most NPOS = 16 * PTN positions
+    static constexpr int NPOS = 16 * PTN;            // position capacity (the real count is kp.npos)
+    static constexpr int PT = PTN;                   // position tiles per board (MFMA N)
     static constexpr int TT = NB * PT;               // position tiles per wave (all boards)
     static constexpr int CT = F / 64;                // co tiles per wave (MFMA M)
     static constexpr int KC = F / 32;                // k-steps per tap
     static constexpr int CPR = F / 8;                // 16-byte chunks of channels per row
-    static constexpr int HALF = ((CPR + 14) * 16 + 255) & ~255;   // one part's rotated chunks
+    // Split precision with F = 128 (16 chunks, 256 B per part): the rotation wraps inside the
+    // 256-byte row (WRAP), so hi + lo fit 512 bytes and two boards fit a workgroup's LDS (k-step
+    // offsets then need an add + and per read: measured slower for the bf16 kernels, which keep
+    // rows with room for the rotated chunks without wrap-around, profiles/r02h_kernel_variants_*)
+    static constexpr bool WRAP = CPR == 16 && P2 == 2;
+    static constexpr int HALF = WRAP ? 256 : ((CPR + 14) * 16 + 255) & ~255;   // one part's row
     static constexpr int ROWS = P2 * HALF;           // LDS row stride: hi part, then lo part
-    static constexpr int ACT_BYTES = (NPOS + 1) * ROWS;           // + one all-zero row
+    static constexpr int ACT_BYTES = (NPOS + 1) * ROWS;           // + one all-zero row (at row kp.npos)
     // k-steps per ring stage and the ring's VGPR budget: F = 256 (4 co tiles per wave, 16 weight
     // VGPRs per k-step) streams single k-steps through a 64-VGPR ring so the accumulators, the
     // residual and the B fragments still fit the 512 registers of a wave without spilling
@@ -117,16 +131,25 @@ struct Geo {
     static constexpr int R = ring_depth(NST, KS, NFR, CT >= 4 ? 64 : 96);
     static constexpr int LPS = KS * NFR;             // weight loads per stage per lane
     // Single-image mode: when two ping-pong images (+ bias table) do not fit the 160 KB of LDS
-    // (F = 256 on 10x10 / 13x13 boards), one image is overwritten in place: every conv's MFMAs
+    // (F = 256 on 10x10 / 13x13 boards), or the registers are nearly full anyway (large boards:
+    // the single-image epilogue keeps fewer values live), one image is overwritten in place: every conv's MFMAs
     // finish reading it (barrier) before its epilogue writes it.  The input staging and head
     // scratch then alias the image.
-    static constexpr bool SI = 2 * NB * ACT_BYTES + 16 * 1024 > 160 * 1024;
+    // live VGPRs of the trunk loop: weight ring + double-buffered B fragments + accumulators +
+    // residual stream
+    static constexpr int LIVE_VGPRS = R * KS * NFR * 4 + 2 * TT * P2 * 4 + 2 * CT * TT * 4;
+    static constexpr bool SI = 2 * NB * ACT_BYTES + 16 * 1024 > 160 * 1024 || (NB == 1 && LIVE_VGPRS > 330);
     // Global residual: when the fp32 residual stream (+ the accumulators) would need more than 256
     // VGPRs (F = 256 on 13x13: 2 x 176), it lives in a per-workgroup device scratch instead of
     // registers, lane-contiguous (one coalesced 1 KB store / load per wave and tile).
     static constexpr bool RG = CT * TT * 4 * 2 > 256;
+    // Compiler-tracked weight loads: above ~300 live VGPRs (ring + double-buffered B fragments +
+    // accumulators + residual) the register allocator moves values between VGPRs and AGPRs, and a
+    // copy of an inline-asm load's destination could be taken before the data lands; such kernels
+    // (and the single-image ones) issue the ring with ordinary loads, which the compiler waits for.
+    static constexpr bool TRACKED = SI || LIVE_VGPRS > 300 || (P2 == 2 && NB == 2);
     static_assert(F % 64 == 0, "filters must be a multiple of 64");
-    static_assert(P == 1 || (P == 3 && NB == 1 && CT <= 2), "split precision: F <= 128, one board per workgroup");
+    static_assert(P == 1 || (P == 3 && CT <= 2 && (NB == 1 || WRAP)), "split precision: F <= 128");
     static_assert(!SI || NB == 1, "single-image mode takes one board per workgroup");
     static_assert(!RG || SI, "the global residual is implemented for single-image kernels");
     static constexpr int RESID_BYTES = RG ? 4 * CT * TT * 64 * 16 : 0;   // per workgroup
@@ -158,11 +181,12 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 
 __device__ __forceinline__ float bf16_lo(float x) { return x - (float)(__bf16)x; }
 
-template <int F, int H, int W, int P = 1>
-__device__ __forceinline__ void store_act(char* X, int p, int co, f32x4 v) {
-    using G = Geo<F, H, W, 1, P>;
-    if (p < G::NPOS) {
-        char* a = X + p * G::ROWS + (((co >> 3) + swz(p)) << 4) + (co & 7) * 2;
+template <int F, int PTN, int P = 1>
+__device__ __forceinline__ void store_act(char* X, int p, int co, f32x4 v, int npos) {
+    using G = Geo<F, PTN, 1, P>;
+    if (p < npos) {
+        const int chunk = G::WRAP ? (((co >> 3) + swz(p)) & 15) : ((co >> 3) + swz(p));
+        char* a = X + p * G::ROWS + (chunk << 4) + (co & 7) * 2;
         uint2 u;
         u.x = pack2(v[0], v[1]);
         u.y = pack2(v[2], v[3]);
@@ -210,9 +234,9 @@ __device__ __forceinline__ void ring_ready(bf16x8& v) { asm volatile("" : "+v"(v
 
 // ---- trunk -------------------------------------------------------------------------------------
 
-template <int F, int H, int W, int NB, int P>
+template <int F, int PTN, int NB, int P>
 struct Ring {
-    using G = Geo<F, H, W, NB, P>;
+    using G = Geo<F, PTN, NB, P>;
     bf16x8 r[G::R][G::KS][G::NFR];    // fragment f = ct * P2 + part
 };
 
@@ -228,22 +252,22 @@ template <int P2, int ROWB, int FR>
 struct FragOff {
     static constexpr int value = (FR / P2) * 16 * ROWB + (FR % P2) * 64;
 };
-template <int F, int H, int W, int NB, int P, int SLOT, int... FRS>
-__device__ __forceinline__ void ring_issue_k(Ring<F, H, W, NB, P>& ring, int k, uint32_t woff, const char* sb,
+template <int F, int PTN, int NB, int P, int SLOT, int... FRS>
+__device__ __forceinline__ void ring_issue_k(Ring<F, PTN, NB, P>& ring, int k, uint32_t woff, const char* sb,
                                              std::integer_sequence<int, FRS...>) {
-    using G = Geo<F, H, W, NB, P>;
-    if constexpr (G::SI)
+    using G = Geo<F, PTN, NB, P>;
+    if constexpr (G::TRACKED)
         ((ring.r[SLOT][k][FRS] = *(const bf16x8*)(sb + woff + FragOff<G::P2, G::ROWB, FRS>::value)), ...);
     else
         ((ring.r[SLOT][k][FRS] = gload_issue<FragOff<G::P2, G::ROWB, FRS>::value>(woff, sb)), ...);
 }
-template <int F, int H, int W, int NB, int P, int SLOT>
-__device__ __forceinline__ void ring_issue(Ring<F, H, W, NB, P>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
-    using G = Geo<F, H, W, NB, P>;
+template <int F, int PTN, int NB, int P, int SLOT>
+__device__ __forceinline__ void ring_issue(Ring<F, PTN, NB, P>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
+    using G = Geo<F, PTN, NB, P>;
     const int s = gs < gmax ? gs : gmax;
 #pragma unroll
     for (int k = 0; k < G::KS; ++k)
-        ring_issue_k<F, H, W, NB, P, SLOT>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * G::ROWB,
+        ring_issue_k<F, PTN, NB, P, SLOT>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * G::ROWB,
                                            std::make_integer_sequence<int, G::NFR>{});
 }
 
@@ -254,31 +278,45 @@ __device__ __forceinline__ void ring_issue(Ring<F, H, W, NB, P>& ring, const __b
 __device__ __forceinline__ void launder(int& v) { asm volatile("" : "+v"(v)); }
 template <typename T>
 __device__ __forceinline__ void launder_ptr(T*& p) { asm volatile("" : "+v"(p)); }
-template <int F, int H, int W, int P = 1>
-__device__ __forceinline__ int tap_base(int tap, int pt, int lane) {
-    using G = Geo<F, H, W, 1, P>;
+// A lane's B-fragment address for tap `tap`, tile pt: row base + rotated chunk offset of k-step 0.
+// k-step kc reads chunk offset (rot + 64 kc), wrapped to the 256-byte row under WRAP (k-step
+// offsets are then not immediates: one add + and per read).
+struct TapAddr {
+    int row, rot;
+};
+template <int F, int PTN, int P = 1>
+__device__ __forceinline__ TapAddr tap_base(int tap, int pt, int lane, const Board& bd) {
+    using G = Geo<F, PTN, 1, P>;
     const int li = lane & 15, g = lane >> 4;
     const int dy = tap / 3 - 1, dx = tap % 3 - 1;
     const int p = 16 * pt + li;
-    const int y = p / W + dy, x = p % W + dx;
-    const bool ok = p < G::NPOS && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-    const int qv = p + dy * W + dx;
-    return (ok ? qv : G::NPOS) * G::ROWS + ((g + swz(qv)) << 4);
+    const int r = bd.row(p);
+    const int y = r + dy, x = p - r * bd.W + dx;
+    const bool ok = p < bd.npos && (unsigned)y < (unsigned)bd.H && (unsigned)x < (unsigned)bd.W;
+    const int qv = p + dy * bd.W + dx;
+    const int rot = G::WRAP ? (((g + swz(qv)) & 15) << 4) : ((g + swz(qv)) << 4);
+    return TapAddr{(ok ? qv : bd.npos) * G::ROWS, rot};
+}
+template <int F, int PTN, int P = 1>
+__device__ __forceinline__ int tap_offset(const TapAddr& t, int kc) {
+    using G = Geo<F, PTN, 1, P>;
+    return G::WRAP ? t.row + ((t.rot + 64 * kc) & 255) : t.row + t.rot + 64 * kc;
 }
 
 // One 3x3 'same' conv over the NB LDS images at X (board b at X + b*ACT_BYTES):
 // acc[ct][t] = W * X (fp32 accumulate), tile t = b*PT + pt.  gs0 = global stage index of this
 // conv's first stage; on entry stages gs0 .. gs0+R-2 are in flight in ring slots 0..R-2.
-template <int F, int H, int W, int NB, int P, int ST>
-__device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, H, W, NB, P>& ring,
-                                           f32x4 (&acc)[Geo<F, H, W, NB, P>::CT][Geo<F, H, W, NB, P>::TT],
-                                           bf16x8 (&b)[2][Geo<F, H, W, NB, P>::TT][Geo<F, H, W, NB, P>::P2],
-                                           const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane) {
-    using G = Geo<F, H, W, NB, P>;
+template <int F, int PTN, int NB, int P, int ST>
+__device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+                                           f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
+                                           bf16x8 (&b)[2][Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
+                                           const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane,
+                                           const Board& bd) {
+    using G = Geo<F, PTN, NB, P>;
     constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC, P2 = G::P2;
     // refill the slot stage ST-1 consumed with stage ST+R-1, then wait for stage ST
-    ring_issue<F, H, W, NB, P, (ST + R - 1) % R>(ring, wres, woff, gs0 + ST + R - 1, gmax);
-    if constexpr (!G::SI) {
+    ring_issue<F, PTN, NB, P, (ST + R - 1) % R>(ring, wres, woff, gs0 + ST + R - 1, gmax);
+    if constexpr (!G::TRACKED) {
         ring_wait<(R - 1) * G::LPS>();
 #pragma unroll
         for (int k = 0; k < KS; ++k)
@@ -295,7 +333,7 @@ __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, H
             if (kc == 0) launder(lane);
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) {
-                const char* a = X + tap_base<F, H, W, P>(tap, pt, lane) + kc * 64;
+                const char* a = X + tap_offset<F, PTN, P>(tap_base<F, PTN, P>(tap, pt, lane, bd), kc);
 #pragma unroll
                 for (int bb = 0; bb < NB; ++bb)
 #pragma unroll
@@ -328,26 +366,27 @@ __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, H
     }
 }
 
-template <int F, int H, int W, int NB, int P, int... S>
-__device__ __forceinline__ void ring_prime(Ring<F, H, W, NB, P>& ring, const __bf16* wres, uint32_t woff, int gmax,
+template <int F, int PTN, int NB, int P, int... S>
+__device__ __forceinline__ void ring_prime(Ring<F, PTN, NB, P>& ring, const __bf16* wres, uint32_t woff, int gmax,
                                            std::integer_sequence<int, S...>) {
-    (ring_issue<F, H, W, NB, P, S>(ring, wres, woff, S, gmax), ...);
+    (ring_issue<F, PTN, NB, P, S>(ring, wres, woff, S, gmax), ...);
 }
 
-template <int F, int H, int W, int NB, int P, int... ST>
-__device__ __forceinline__ void conv_stages(const char* __restrict__ X, Ring<F, H, W, NB, P>& ring,
-                                            f32x4 (&acc)[Geo<F, H, W, NB, P>::CT][Geo<F, H, W, NB, P>::TT],
-                                            bf16x8 (&b)[2][Geo<F, H, W, NB, P>::TT][Geo<F, H, W, NB, P>::P2],
+template <int F, int PTN, int NB, int P, int... ST>
+__device__ __forceinline__ void conv_stages(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+                                            f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
+                                            bf16x8 (&b)[2][Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
                                             const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane,
-                                            std::integer_sequence<int, ST...>) {
-    (conv_stage<F, H, W, NB, P, ST>(X, ring, acc, b, wres, woff, gs0, gmax, lane), ...);
+                                            const Board& bd, std::integer_sequence<int, ST...>) {
+    (conv_stage<F, PTN, NB, P, ST>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd), ...);
 }
 
-template <int F, int H, int W, int NB, int P>
-__device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, H, W, NB, P>& ring,
-                                        f32x4 (&acc)[Geo<F, H, W, NB, P>::CT][Geo<F, H, W, NB, P>::TT],
-                                        const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane) {
-    using G = Geo<F, H, W, NB, P>;
+template <int F, int PTN, int NB, int P>
+__device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+                                        f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
+                                        const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane,
+                                        const Board& bd) {
+    using G = Geo<F, PTN, NB, P>;
     constexpr int PT = G::PT, TT = G::TT;
 #pragma unroll
     for (int ct = 0; ct < G::CT; ++ct)
@@ -358,23 +397,26 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, H, W
     launder(lane);
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt) {
-        const char* a = X + tap_base<F, H, W, P>(0, pt, lane);
+        const char* a = X + tap_offset<F, PTN, P>(tap_base<F, PTN, P>(0, pt, lane, bd), 0);
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb)
 #pragma unroll
             for (int h = 0; h < G::P2; ++h) b[0][bb * PT + pt][h] = *(const bf16x8*)(a + bb * G::ACT_BYTES + h * G::HALF);
     }
-    conv_stages<F, H, W, NB, P>(X, ring, acc, b, wres, woff, gs0, gmax, lane, std::make_integer_sequence<int, G::NST>{});
+    conv_stages<F, PTN, NB, P>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd,
+                               std::make_integer_sequence<int, G::NST>{});
 }
 
 // NB boards per workgroup of 4 waves; WPE = minimum resident waves per SIMD the register
 // allocation must allow (amdgpu_waves_per_eu), i.e. WPE workgroups per CU.
-template <int F, int H, int W, int NB, int WPE, int P>
+template <int F, int PTN, int NB, int WPE, int P>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 trunk_kernel(const KParams kp) {
-    using G = Geo<F, H, W, NB, P>;
+    using G = Geo<F, PTN, NB, P>;
     constexpr int P2 = G::P2;
-    constexpr int NPOS = G::NPOS, PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, kThreads = 256;
+    constexpr int PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, kThreads = 256;
+    const int NPOS = kp.npos, H = kp.H, W = kp.W;     // the board (NPOS <= G::NPOS)
+    const Board bd{H, W, NPOS, kp.wmagic};
     constexpr int ACT = G::ACT_BYTES;
 
     constexpr bool SI = G::SI, RG = G::RG;
@@ -398,8 +440,8 @@ trunk_kernel(const KParams kp) {
     // prime the weight ring: stages 0 .. R-2 of the trunk stream
     const uint32_t woff = (uint32_t)((co_base + li) * G::ROWB + 16 * g);   // lane's fragment bytes within a k-step
     const int gmax = 2 * kp.B * G::NST - 1;
-    Ring<F, H, W, NB, P> ring;
-    if (kp.B > 0) ring_prime<F, H, W, NB, P>(ring, kp.wres, woff, gmax, std::make_integer_sequence<int, R - 1>{});
+    Ring<F, PTN, NB, P> ring;
+    if (kp.B > 0) ring_prime<F, PTN, NB, P>(ring, kp.wres, woff, gmax, std::make_integer_sequence<int, R - 1>{});
 
     f32x4 acc[CT][TT];
     f32x4 resid[RG ? 1 : CT][RG ? 1 : TT];
@@ -431,7 +473,8 @@ trunk_kernel(const KParams kp) {
         __syncthreads();
         for (int i = tid; i < NPOS * 9; i += kThreads) {
             const int p = i / 9, tap = i - (i / 9) * 9;
-            const int y = p / W + tap / 3 - 1, x = p % W + tap % 3 - 1;
+            const int r = bd.row(p);
+            const int y = r + tap / 3 - 1, x = p - r * W + tap % 3 - 1;
             if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
                 const float* src = sin + y * W + x;
                 for (int c = 0; c < C; ++c) {
@@ -490,7 +533,7 @@ trunk_kernel(const KParams kp) {
                 if constexpr (RG) rg[(ct * TT + bb * PT + pt) * 64] = v;
                 else resid[ct][bb * PT + pt] = v;
                 acc[ct][bb * PT + pt] = v;    // the heads read acc when there is no residual block
-                store_act<F, H, W, P>(X0 + bb * ACT, 16 * pt + li, co, v);
+                store_act<F, PTN, P>(X0 + bb * ACT, 16 * pt + li, co, v, NPOS);
             }
         }
         __syncthreads();    // scratch is reused by the next board
@@ -508,7 +551,7 @@ trunk_kernel(const KParams kp) {
         for (int cv = 0; cv < 2 * kp.B; ++cv) {
             const bool second = cv & 1;
             const float* bt = btab + cv * F;
-            conv3x3<F, H, W, NB, P>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane);
+            conv3x3<F, PTN, NB, P>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane, bd);
             __syncthreads();    // every wave has finished reading the image it is about to overwrite
             // residual tile addresses are formed here, not hoisted out of the loop (44 x 64-bit)
             f32x4* rgc = rg;
@@ -536,7 +579,7 @@ trunk_kernel(const KParams kp) {
                         else resid[ct][t] = v;
                         acc[ct][t] = v;
                     }
-                    store_act<F, H, W, P>(X0, 16 * t + li, co, v);
+                    store_act<F, PTN, P>(X0, 16 * t + li, co, v, NPOS);
                 }
             }
             __syncthreads();
@@ -546,7 +589,7 @@ trunk_kernel(const KParams kp) {
         const float* b_a = btab + (2 * blk) * F;
         const float* b_b = b_a + F;
 
-        conv3x3<F, H, W, NB, P>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane);
+        conv3x3<F, PTN, NB, P>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -558,12 +601,12 @@ trunk_kernel(const KParams kp) {
                 v[1] = act_fn(v[1] + bias.y, kp.leaky);
                 v[2] = act_fn(v[2] + bias.z, kp.leaky);
                 v[3] = act_fn(v[3] + bias.w, kp.leaky);
-                store_act<F, H, W, P>(X1 + (t / PT) * ACT, 16 * (t % PT) + li, co, v);
+                store_act<F, PTN, P>(X1 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);
             }
         }
         __syncthreads();
 
-        conv3x3<F, H, W, NB, P>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane);
+        conv3x3<F, PTN, NB, P>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane, bd);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -578,13 +621,13 @@ trunk_kernel(const KParams kp) {
                 v[3] = act_fn(v[3] + bias.w + r[3], kp.leaky);
                 resid[ct][t] = v;
                 acc[ct][t] = v;
-                store_act<F, H, W, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v);
+                store_act<F, PTN, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);
             }
         }
         __syncthreads();
     }
     // the clamped tail stages are never consumed: land them before their registers are released
-    if (!SI && kp.B > 0) {
+    if (!G::TRACKED && kp.B > 0) {
         ring_wait<0>();
 #pragma unroll
         for (int s = 0; s < R; ++s)
@@ -652,6 +695,7 @@ trunk_kernel(const KParams kp) {
 // P_r or VH) for every board of the workgroup; the k-major weights are read coalesced, each once
 // per workgroup, and the features come from LDS as one broadcast float4 per k (k-major, board-minor
 // image).  Each board's sums run in a fixed k order: outputs are independent of batch composition.
+#ifdef GZNN_DEFINE_HEADS_KERNEL   // defined in one translation unit (gz_nn.hip)
 __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
     constexpr int BPW = kHeadBoards;
     static_assert(BPW == 4, "one float4 of features per k, one softmax wave per board");
@@ -755,6 +799,8 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
     }
     (void)red;
 }
+
+#endif
 
 __host__ inline int heads_lds_bytes(int npos, int R, int maxP, int VH) {
     const int FS = (2 * R + 1) * npos;

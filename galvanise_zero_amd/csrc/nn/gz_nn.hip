@@ -3,7 +3,9 @@
 // Host side: parses the canonical Keras-order float32 blob (galvanise_zero_amd/nn/desc.py
 // weight_spec), folds inference BatchNorm (eps 1e-3, model.py:21-22) into the preceding conv,
 // packs conv kernels into bf16 MFMA fragment order and uploads one device allocation.
+#define GZNN_DEFINE_HEADS_KERNEL
 #include "forward_kernel.h"
+#include "trunk_variants.h"
 #include "../../../include/gzero_nn.h"
 
 #include <hip/hip_runtime.h>
@@ -47,6 +49,7 @@ struct gz_net {
     } small, large;                // launches below / from large_min_rows rows
     int large_min_rows = 1 << 30;
     int p2 = 1;                    // bf16 parts per operand: 1 (bf16) or 2 (split precision)
+    int fpad = 0;                  // filters rounded up to the compiled 64 / 128 / 256 (zero channels)
     bool has_weights = false;
 
     char* dmem = nullptr;          // all weights, one allocation
@@ -70,49 +73,10 @@ struct gz_net {
 
 extern "C" const char* gz_nn_last_error(void) { return g_err.c_str(); }
 
-// ---- kernel instantiations ----------------------------------------------------------------
-// Variants: NB = boards per workgroup (weight-fragment reuse factor), WPE = minimum resident
-// waves per SIMD the register budget must allow (= workgroups per CU).  The default per geometry
-// is the measured fastest ("forward kernel"); GZ_KERNEL_VARIANT=<NB><WPE> (e.g. "22")
-// overrides it for experiments.
-struct KernelChoice {
-    const void* fn = nullptr;
-    int act_bytes = 0;
-    int nb = 1;
-    bool single_image = false;
-    int resid_bytes = 0;           // global residual scratch per workgroup (0: registers)
-};
-
-template <int F, int H, int W, int NB, int WPE, int P = 1>
-static KernelChoice kernel_for() {
-    KernelChoice k;
-    k.fn = (const void*)&trunk_kernel<F, H, W, NB, WPE, P>;
-    k.act_bytes = Geo<F, H, W, NB, P>::ACT_BYTES;
-    k.nb = NB;
-    k.single_image = Geo<F, H, W, NB, P>::SI;
-    k.resid_bytes = Geo<F, H, W, NB, P>::RESID_BYTES;
-    return k;
-}
-
-template <int F, int H, int W>
-static KernelChoice variants(int v, int precision) {
-    if (precision == GZ_PRECISION_SPLIT) {
-        // split precision: hi + lo images, one board per workgroup (LDS), F <= 128
-        if constexpr (F <= 128) {
-            if constexpr (2 * Geo<F, H, W, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024)
-                return v == 11 ? kernel_for<F, H, W, 1, 1, 3>() : KernelChoice{};
-        }
-        return KernelChoice{};
-    }
-    if constexpr (4 * Geo<F, H, W, 1>::ACT_BYTES + 16 * 1024 > 160 * 1024) {   // large boards / filters: one board per workgroup only
-        return v == 11 ? kernel_for<F, H, W, 1, 1>() : KernelChoice{};
-    } else switch (v) {
-        case 11: return kernel_for<F, H, W, 1, 1>();
-        case 12: return kernel_for<F, H, W, 1, 2>();
-        case 21: return kernel_for<F, H, W, 2, 1>();
-        default: return KernelChoice{};
-    }
-}
+// ---- kernel instantiations: trunk_variants.h (per padded filter count and position tiles) ----------
+// Variants: NB = boards per workgroup (weight-fragment reuse factor), WPE = minimum resident waves
+// per SIMD the register budget must allow (= workgroups per CU).  GZ_KERNEL_VARIANT=<NB><WPE>
+// (e.g. "12") overrides the per-launch choice for experiments.
 
 // Measured on MI355X (profiles/r01c_kernel_variants.txt): one board per workgroup with the whole
 // register file (11) is fastest while the launch has fewer boards than ~1.5x the CU count; from
@@ -124,17 +88,9 @@ static KernelChoice variants(int v, int precision) {
 constexpr int kSmallVariant = 11, kLargeVariant = 21, kLargeMinRows = 257;
 constexpr int kCUs = 256;
 
-static KernelChoice select_kernel(int F, int H, int W, int v, int precision) {
-#define GZ_CASE(F_, H_, W_) \
-    if (F == F_ && H == H_ && W == W_) return variants<F_, H_, W_>(v, precision);
-    GZ_CASE(64, 6, 6)
-    GZ_CASE(128, 6, 6)
-    GZ_CASE(64, 8, 8)
-    GZ_CASE(128, 8, 8)
-    GZ_CASE(256, 10, 10)
-    GZ_CASE(256, 13, 13)
-#undef GZ_CASE
-    return KernelChoice{};
+static KernelChoice select_kernel(int fpad, int pt, int v, int precision) {
+    if (pt < 1 || pt > kMaxPT) return KernelChoice{};
+    return trunk_variant(fpad, pt, v, precision);
 }
 
 // ---- bf16 (round to nearest even) -------------------------------------------------------------
@@ -171,8 +127,14 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         vs = vl = atoi(e);
         min_large = 1 << 30;
     }
-    const KernelChoice kc = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vs, precision);
-    KernelChoice kl = select_kernel(d.cnn_filter_size, d.input_columns, d.input_rows, vl, precision);
+    // kernels are compiled per padded filter count and position-tile count; the board's H and W
+    // are kernel arguments (H = input_columns, W = input_rows: bases.py:104-121)
+    const int fpad = padded_filters(d.cnn_filter_size);
+    const int npos_ = d.input_columns * d.input_rows;
+    const int pt = (npos_ + 15) / 16;
+    if (d.input_rows > 32 || npos_ >= 1024) { fail("board too large"); return nullptr; }
+    const KernelChoice kc = select_kernel(fpad, pt, vs, precision);
+    KernelChoice kl = select_kernel(fpad, pt, vl, precision);
     if (kc.fn && !kl.fn && vl != vs) {   // geometries with a single (one board per workgroup) variant
         kl = kc;
         min_large = 1 << 30;
@@ -188,6 +150,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     net->device = device;
     net->large_min_rows = min_large;
     net->p2 = precision == GZ_PRECISION_SPLIT ? 2 : 1;
+    net->fpad = fpad;
     net->K0 = ((9 * d.input_channels + 31) / 32) * 32;
     net->nweights = spec_count(d);
     int maxP = 0;
@@ -203,7 +166,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         t.btab_off = c.single_image ? align16(std::max(c.act_bytes, scr))
                                     : c.nb * c.act_bytes + std::max(c.nb * c.act_bytes, scr);
         t.resid_bytes = c.resid_bytes;
-        t.smem = t.btab_off + bias_table_bytes(d.cnn_filter_size, d.residual_layers);
+        t.smem = t.btab_off + bias_table_bytes(fpad, d.residual_layers);
         return t;
     };
     net->small = trunk(kc);
@@ -221,6 +184,9 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     kp.value_sigmoid = d.value_sigmoid;
     kp.maxP = maxP;
     kp.npos = npos;
+    kp.H = d.input_columns;
+    kp.W = d.input_rows;
+    kp.wmagic = (65536 + kp.W - 1) / kp.W;
     for (int r = 0; r < d.role_count; ++r) kp.P[r] = d.policy_dist_count[r];
 
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&net->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -295,16 +261,19 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     if (count != net->nweights)
         return fail("weight count mismatch: got " + std::to_string(count) + " expected " + std::to_string(net->nweights));
     const gz_net_desc& d = net->d;
+    // F = the model's filters; FP = the kernel's (padded with zero channels: zero weights and zero
+    // folded bias keep them at 0 through every ReLU and residual add)
     const int F = d.cnn_filter_size, C = d.input_channels, B = d.residual_layers, R = d.role_count;
-    const int HW = d.input_columns * d.input_rows, K0 = net->K0, KC = F / 32;
+    const int FP = net->fpad;
+    const int HW = d.input_columns * d.input_rows, K0 = net->K0, KC = FP / 32;
     const int HC = 2 * R + 1;
     const float eps = 1e-3f;
 
     // host images
     const int P2 = net->p2;
-    std::vector<uint16_t> w0((size_t)K0 * F, 0), w0lo(P2 == 2 ? (size_t)K0 * F : 0, 0);
-    std::vector<float> b0(F);
-    std::vector<uint16_t> wres((size_t)P2 * 2 * B * 9 * F * F);
+    std::vector<uint16_t> w0((size_t)K0 * FP, 0), w0lo(P2 == 2 ? (size_t)K0 * FP : 0, 0);
+    std::vector<float> b0(FP, 0.f);
+    std::vector<uint16_t> wres((size_t)P2 * 2 * B * 9 * FP * FP, 0);
     // split precision: x = hi + lo, hi = bf16(x), lo = bf16(x - hi)
     auto lo_of = [](float v) {
         const uint16_t h = f2bf(v);
@@ -313,8 +282,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
         std::memcpy(&hf, &u, 4);
         return f2bf(v - hf);
     };
-    std::vector<float> bres((size_t)2 * B * F);
-    std::vector<float> wh((size_t)HC * F), bh(HC, 0.f);
+    std::vector<float> bres((size_t)2 * B * FP, 0.f);
+    std::vector<float> wh((size_t)HC * FP, 0.f), bh(HC, 0.f);
 
     Cursor cur{blob};
     // BN after a conv with bias cb (legacy model files): gamma*(conv + cb - mean)/sqrt(var+eps) + beta
@@ -342,8 +311,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
             for (int k = 0; k < 9 * C; ++k) {
                 const int tap = k / C, c = k % C;
                 const float v = w[((size_t)tap * C + c) * F + co] * s[co];
-                w0[((size_t)(k / 32) * F + co) * 32 + (k % 32)] = f2bf(v);
-                if (P2 == 2) w0lo[((size_t)(k / 32) * F + co) * 32 + (k % 32)] = lo_of(v);
+                w0[((size_t)(k / 32) * FP + co) * 32 + (k % 32)] = f2bf(v);
+                if (P2 == 2) w0lo[((size_t)(k / 32) * FP + co) * 32 + (k % 32)] = lo_of(v);
             }
         }
     }
@@ -352,13 +321,13 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
         const float* w = cur.take((size_t)9 * F * F);
         const float* cb = conv_bias(F);
         bn_fold(F, s, bb, cb);
-        uint16_t* dst = wres.data() + (size_t)P2 * conv * 9 * F * F;
+        uint16_t* dst = wres.data() + (size_t)P2 * conv * 9 * FP * FP;
         for (int co = 0; co < F; ++co) {
-            bres[(size_t)conv * F + co] = bb[co];
+            bres[(size_t)conv * FP + co] = bb[co];
             for (int tap = 0; tap < 9; ++tap)
                 for (int ci = 0; ci < F; ++ci) {
                     const float v = w[((size_t)tap * F + ci) * F + co] * s[co];
-                    const size_t o = ((((size_t)tap * KC + ci / 32) * F + co) * P2) * 32 + (ci % 32);
+                    const size_t o = ((((size_t)tap * KC + ci / 32) * FP + co) * P2) * 32 + (ci % 32);
                     dst[o] = f2bf(v);
                     if (P2 == 2) dst[o + 32] = lo_of(v);
                 }
@@ -370,7 +339,7 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
         const float* cb = conv_bias(2);
         bn_fold(2, s, bb, cb);
         for (int c = 0; c < 2; ++c) {
-            for (int f = 0; f < F; ++f) wh[(size_t)(2 * r + c) * F + f] = w[(size_t)f * 2 + c] * s[c];
+            for (int f = 0; f < F; ++f) wh[(size_t)(2 * r + c) * FP + f] = w[(size_t)f * 2 + c] * s[c];
             bh[2 * r + c] = bb[c];
         }
         pdense[r] = cur.take((size_t)2 * HW * d.policy_dist_count[r]);
@@ -385,7 +354,7 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
             vs = s[0];
             vb = bb[0];
         }
-        for (int f = 0; f < F; ++f) wh[(size_t)(2 * R) * F + f] = w[f] * vs;
+        for (int f = 0; f < F; ++f) wh[(size_t)(2 * R) * FP + f] = w[f] * vs;
         bh[2 * R] = vb;
     }
     const float* vhw = cur.take((size_t)HW * d.value_hidden_size);

@@ -1,0 +1,77 @@
+// Registry of the compiled trunk-kernel instantiations (one translation unit per filter count,
+// trunk_f64.hip / trunk_f128.hip / trunk_f256.hip, so they compile in parallel).
+//
+// A trunk kernel is compiled per (F, PT): F = filters rounded up to 64 / 128 / 256 (the host pads
+// other filter counts with zero channels), PT = position tiles of 16 (boards of up to 16 * PT
+// positions, H and W given at run time).  Variants per geometry: NB boards per workgroup x WPE
+// workgroups per CU ("11", "12", "21"), and the split-precision kernel (P = 3, one board per
+// workgroup, boards of up to 64 positions).
+#pragma once
+
+#include "forward_kernel.h"
+
+namespace gznn {
+
+struct KernelChoice {
+    const void* fn = nullptr;
+    int act_bytes = 0;
+    int nb = 1;
+    bool single_image = false;
+    int resid_bytes = 0;           // global residual scratch per workgroup (0: registers)
+};
+
+template <int F, int PTN, int NB, int WPE, int P = 1>
+KernelChoice kernel_for() {
+    KernelChoice k;
+    k.fn = (const void*)&trunk_kernel<F, PTN, NB, WPE, P>;
+    k.act_bytes = Geo<F, PTN, NB, P>::ACT_BYTES;
+    k.nb = NB;
+    k.single_image = Geo<F, PTN, NB, P>::SI;
+    k.resid_bytes = Geo<F, PTN, NB, P>::RESID_BYTES;
+    return k;
+}
+
+// precision 3: split (hi / lo) operands; otherwise bf16.  v = NB * 10 + WPE.
+template <int F, int PTN>
+KernelChoice variants(int v, int precision) {
+    if (precision == 3) {
+        if constexpr (F <= 128 && PTN <= 4) {
+            if constexpr (2 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024) {
+                if (v == 11) return kernel_for<F, PTN, 1, 1, 3>();
+                // two boards per workgroup (F = 128: 256-byte wrapped rows, hi + lo in 512 bytes)
+                if constexpr (Geo<F, PTN, 1, 3>::WRAP && 4 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024)
+                    if (v == 21) return kernel_for<F, PTN, 2, 1, 3>();
+            }
+        }
+        return KernelChoice{};
+    }
+    if constexpr (4 * Geo<F, PTN, 1>::ACT_BYTES + 16 * 1024 > 160 * 1024) {   // one board per workgroup only
+        return v == 11 ? kernel_for<F, PTN, 1, 1>() : KernelChoice{};
+    } else {
+        switch (v) {
+            case 11: return kernel_for<F, PTN, 1, 1>();
+            case 12: if constexpr (PTN == 4) return kernel_for<F, PTN, 1, 2>(); else return KernelChoice{};
+            case 21:   // (not where the two boards' tiles would spill registers)
+                if constexpr (Geo<F, PTN, 2>::LIVE_VGPRS <= 300) return kernel_for<F, PTN, 2, 1>();
+                else return KernelChoice{};
+            default: return KernelChoice{};
+        }
+    }
+}
+
+KernelChoice trunk_variant_f64(int pt, int v, int precision);
+KernelChoice trunk_variant_f128(int pt, int v, int precision);
+KernelChoice trunk_variant_f256(int pt, int v, int precision);
+
+// padded filter count and position tiles of a board; 0 when not compiled
+inline int padded_filters(int F) { return F <= 64 ? 64 : F <= 128 ? 128 : F <= 256 ? 256 : 0; }
+constexpr int kMaxPT = 11;   // boards of up to 176 positions (13 x 13)
+
+inline KernelChoice trunk_variant(int fpad, int pt, int v, int precision) {
+    if (fpad == 64) return trunk_variant_f64(pt, v, precision);
+    if (fpad == 128) return trunk_variant_f128(pt, v, precision);
+    if (fpad == 256) return trunk_variant_f256(pt, v, precision);
+    return KernelChoice{};
+}
+
+}  // namespace gznn

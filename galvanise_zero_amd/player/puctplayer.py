@@ -61,9 +61,11 @@ class PUCTPlayer(object):
         if self.poller is not None:
             self.poller.player_reset(0)
 
-    def on_meta_gaming(self, match, finish_time=-1):
-        """puctplayer.py:33-63."""
-        self.match = match
+    def on_meta_gaming(self, finish_time=-1):
+        """puctplayer.py:33-63.  As in ggplib's MatchPlayer, the match is set on the player
+        (``player.match = ...``) before meta-gaming."""
+        match = self.match
+        assert match is not None, "set player.match before on_meta_gaming (MatchPlayer protocol)"
         if self.sm is None or "*" in self.conf.generation:
             self.sm = get_sm(match.game)
             if self.nn is None:
@@ -121,7 +123,8 @@ def play_match(game, players, max_moves=500):
     (goal values, moves).  Both players see every joint move (the GGP protocol's play message)."""
     matches = [Match(game, r) for r in range(2)]
     for p, m in zip(players, matches):
-        p.on_meta_gaming(m)
+        p.match = m
+        p.on_meta_gaming(-1)
     moves = []
     ref = matches[0]
     while not ref.is_terminal() and len(moves) < max_moves:

@@ -202,3 +202,60 @@ def test_batch_invariance_fp32(name, hip_device):
     perm = np.random.default_rng(0).permutation(300)[:37]
     for a, b in zip(full, net.forward(x[perm])):
         assert np.array_equal(a[perm], b)
+
+
+# ---- generic geometry: the reference's own network templates on every BASELINE game -----------
+# templates.nn_model_config_template (reference templates.py:21-71): small F=64 x 5 blocks,
+# medium F=96 x 5, large F=96 x 10 (F=96 runs on the 128-filter kernels with zero channels); the
+# board is a kernel argument (kernels compiled per 16-position tile count).
+TOL_BF16_GEOM = (9e-2, 1.8e-2)   # bf16 mode: 3 x the worst measured over these 15 nets (max 0.030, mean 0.0061; profiles/r02g_gpu_tests.log)
+GEOM_GAMES = ["breakthroughSmall", "breakthrough", "reversi", "hexLG13", "amazons_10x10"]
+
+
+def _template_desc(game, hint):
+    from galvanise_zero_amd.defs import templates
+    from galvanise_zero_amd.nn.bases import GdlBasesTransformer
+    from galvanise_zero_amd.nn.network import desc_from_conf
+    from galvanise_zero_amd.sm import get_sm
+    gen = templates.default_generation_desc(game, num_previous_states=1)
+    t = GdlBasesTransformer(get_sm(game), gen)
+    return desc_from_conf(templates.nn_model_config_template(game, hint, t), gen)
+
+
+@pytest.mark.parametrize("hint", ["small", "medium", "large"])
+@pytest.mark.parametrize("game", GEOM_GAMES)
+def test_template_geometries(game, hint, hip_device):
+    from galvanise_zero_amd._native import HipNet
+    desc = _template_desc(game, hint)
+    w = random_weights(desc, 7919, bias_std=0.2, res_gamma=0.15 if desc.residual_layers > 6 else 1.0)
+    x = random_planes(desc, 9, 31)
+    ref = nn_ref.forward(desc, w, x)
+    modes = [("bf16", TOL_BF16_GEOM)]
+    if desc.hw <= 64:
+        modes.append(("fp32", TOL_FP32))
+    for precision, tol in modes:
+        net = HipNet(desc, hip_device, precision)
+        net.set_weights(to_blob(w))
+        for i, (g, r) in enumerate(zip(net.forward(x), ref)):
+            er = _err(g, r)
+            print("geom %s/%s %s F=%d B=%d out%d vs_ref max %.3g mean %.3g" % (game, hint, precision, desc.cnn_filter_size,
+                                                                             desc.residual_layers, i, er[0], er[1]))
+            assert np.all(np.isfinite(g)) and g.shape == r.shape
+            assert er[0] <= tol[0] and er[1] <= tol[1], (game, hint, precision, i, er)
+
+
+@pytest.mark.parametrize("variant", ["11", "21"])
+def test_kernel_variants_identical_fp32(variant, hip_device, monkeypatch):
+    """The split-precision kernels (one or two boards per workgroup) compute every row identically."""
+    from galvanise_zero_amd._native import HipNet
+    desc = VARIANTS["cfg2"]
+    x = random_planes(desc, 33, 4)
+    w = to_blob(random_weights(desc, 5, bias_std=0.2))
+    net = HipNet(desc, hip_device, "fp32")
+    net.set_weights(w)
+    base = net.forward(x)
+    monkeypatch.setenv("GZ_KERNEL_VARIANT", variant)
+    vnet = HipNet(desc, hip_device, "fp32")
+    vnet.set_weights(w)
+    for a, b in zip(base, vnet.forward(x)):
+        assert np.array_equal(a, b)

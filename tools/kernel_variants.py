@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--configs", default="1,2,3")
     ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     args = ap.parse_args()
     batches = [int(b) for b in args.batches.split(",")]
     for cfg in [int(c) for c in args.configs.split(",")]:
@@ -40,7 +41,7 @@ def main():
             else:
                 os.environ["GZ_KERNEL_VARIANT"] = v
             try:
-                net = HipNet(desc, 0)
+                net = HipNet(desc, 0, args.precision)
             except RuntimeError as e:
                 print("cfg%d variant %s: n/a (%s)" % (cfg, v, e), flush=True)
                 continue
@@ -56,8 +57,8 @@ def main():
                 if n not in base:
                     base[n] = out
                 diff = max(float(np.abs(a - b).max()) for a, b in zip(out, base[n]))
-                print("cfg%d variant %s N=%5d  %8.3f ms  %7.1f TFLOP/s  %9.0f evals/s  maxdiff %.2e"
-                      % (cfg, v, n, ms, fl * n / ms / 1e9, n / ms * 1e3, diff), flush=True)
+                print("cfg%d %s variant %s N=%5d  %8.3f ms  %7.1f TFLOP/s  %9.0f evals/s  maxdiff %.2e"
+                      % (cfg, args.precision, v, n, ms, fl * n / ms / 1e9, n / ms * 1e3, diff), flush=True)
             net.close()
 
 
