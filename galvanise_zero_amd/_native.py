@@ -54,7 +54,12 @@ class GzNetDesc(ctypes.Structure):
                 ("conv_bias", ctypes.c_int),
                 ("value_bn", ctypes.c_int),
                 ("value_sigmoid", ctypes.c_int),
-                ("precision", ctypes.c_int)]
+                ("precision", ctypes.c_int),
+                ("resnet_v2", ctypes.c_int),
+                ("initial_kernel", ctypes.c_int),
+                ("initial_bn", ctypes.c_int),
+                ("se_units", ctypes.c_int),
+                ("global_pooling_value", ctypes.c_int)]
 
 GZ_PRECISION_BF16 = 1
 GZ_PRECISION_SPLIT = 3
@@ -119,6 +124,11 @@ def make_net_desc(desc, precision=GZ_PRECISION_BF16):
     d.value_bn = int(getattr(desc, "value_bn", False))
     d.value_sigmoid = int(getattr(desc, "value_sigmoid", False))
     d.flatten_nchw = int(desc.flatten_nchw)
+    d.resnet_v2 = int(getattr(desc, "resnet_v2", False))
+    d.initial_kernel = int(desc.initial_kernel) if hasattr(desc, "initial_kernel") else 0
+    d.initial_bn = int(getattr(desc, "initial_bn", True))
+    d.se_units = int(getattr(desc, "se_units", 0))
+    d.global_pooling_value = int(getattr(desc, "global_pooling_value", False))
     return d
 
 

@@ -1,8 +1,10 @@
-// Forward of the v1 residual policy/value CNN for gfx950 (MI355X): two launches per batch.
+// Forward of the residual policy/value CNN (v1, and v2 pre-activation with squeeze-excite and the
+// global-pooling value head) for gfx950 (MI355X): two launches per batch.
 //
 // trunk_kernel: one workgroup (4 waves) evaluates NB boards through the whole trunk:
 //   planes (fp32 NCHW, HBM or pinned host) -> im2col in LDS -> initial conv -> B residual blocks
-//   -> the heads' 1x1 convs -> per-board head features (fp32) to a device scratch.
+//   -> the heads' 1x1 convs (+ the trunk's per-channel means for a pooling value head) -> per-board
+//   head features (fp32) to a device scratch.
 //   Trunk activations never leave the CU: the bf16 copy that feeds the next conv lives in LDS
 //   (two ping-pong images per board), the fp32 residual stream lives in the MFMA accumulators.
 // heads_kernel: one workgroup takes BPW boards' features and applies the policy Dense + softmax
@@ -43,6 +45,7 @@ namespace gznn {
 constexpr int kMaxRoles = 4;
 constexpr int kMaxSegments = 32;
 constexpr int kHeadBoards = 4;     // boards per heads_kernel workgroup (one softmax wave per board)
+constexpr int kMaxSE = 64;         // squeeze-excite units
 
 // One contiguous run of boards of a launch: its planes and outputs may live anywhere the device
 // can address (HBM, or pinned host memory of a game pool: zero-copy gather / scatter).
@@ -70,7 +73,11 @@ struct KParams {
     const float* vhb;        // [VH]
     const float* vdw;        // value dense [VH][V]
     const float* vdb;        // [V]
-    float* feat;             // scratch [n][HC*HW]: head features in flatten order (trunk -> heads)
+    // v2 (pre-activation) blocks, model.py:78-151
+    const float* pre;        // [B][2][F]: BN before each block's first conv, as scale / shift
+    const float* sew1;       // squeeze-excite compress [B][F][S] (Keras [in][out], padded channels 0)
+    const float* sew2;       // squeeze-excite gating [B][S][F]
+    float* feat;             // scratch [n][FS]: head features in flatten order (trunk -> heads)
     f32x4* resid;            // global-residual variants only: [grid][4 waves][CT*TT][64 lanes]
     int n;                  // boards in this launch
     int nseg;                // segments (>= 1), ascending row0, seg[0].row0 == 0
@@ -79,7 +86,14 @@ struct KParams {
     int C, K0, B, R, VH, V, leaky, flatten_nchw, maxP, npos;
     int H, W, wmagic;        // board rows / columns; wmagic = ceil(65536 / W) (Board::div)
     int value_sigmoid;       // legacy model files: independent sigmoid per value output
+    int v2;                  // pre-activation blocks: stream s += conv2(act(BN(conv1(act(BN(s)))))) [* SE gate]
+    int k0taps;              // initial conv taps: 9 (3x3) or 1 (1x1, v2)
+    int init_act;            // activation after the initial conv (0: v2 files with a bare initial conv)
+    int S;                   // squeeze-excite units (0: none), <= kMaxSE
+    int gapF;                // pooling value head: the model's F channel means precede the value conv
+    int FS;                  // head features per board: 2R*npos (policy) + gapF + npos (value)
     int btab_off;            // LDS byte offset of the trunk bias table
+    int se_off;              // LDS byte offset of the squeeze-excite scratch
     int P[kMaxRoles];
 };
 
@@ -169,6 +183,8 @@ __host__ __device__ inline int trunk_scratch_bytes(int npos, int C, int K0, int 
     return in_stage > heads ? in_stage : heads;
 }
 __host__ __device__ inline int bias_table_bytes(int F, int B) { return align16((2 * B) * F * 4); }
+// squeeze-excite scratch: per board the channel means [F] and the compressed units [kMaxSE]
+__host__ __device__ inline int se_scratch_bytes(int F, int NB) { return NB * (F + kMaxSE) * 4; }
 
 __device__ __forceinline__ float act_fn(float v, int leaky) {
     return v > 0.f ? v : (leaky ? 0.03f * v : 0.f);
@@ -407,11 +423,95 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN,
                                std::make_integer_sequence<int, G::NST>{});
 }
 
-// NB boards per workgroup of 4 waves; WPE = minimum resident waves per SIMD the register
-// allocation must allow (amdgpu_waves_per_eu), i.e. WPE workgroups per CU.
-template <int F, int PTN, int NB, int WPE, int P>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
-trunk_kernel(const KParams kp) {
+// Per-board channel sums over the board's positions of the wave's accumulator tiles: lane group g
+// (lanes 16g .. 16g+15) ends with the sums of channels co_base + 16ct + 4g + r in every lane.  The
+// order (tiles ascending, then a butterfly over the 16 lanes) depends only on the board.
+template <int F, int PTN, int NB, int P>
+__device__ __forceinline__ f32x4 board_channel_sum(const f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
+                                                   int ct, int bb, int li, int npos) {
+    using G = Geo<F, PTN, NB, P>;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int pt = 0; pt < G::PT; ++pt)
+        if (16 * pt + li < npos) {
+            const f32x4 v = acc[ct][bb * G::PT + pt];
+            s[0] += v[0]; s[1] += v[1]; s[2] += v[2]; s[3] += v[3];
+        }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], o, 64);
+    return s;
+}
+
+// Squeeze-excite gate of v2 block `blk` (model.py:101-126) applied in place to the conv2 output in
+// acc: per board, channel means -> Dense(S) relu -> Dense(F) sigmoid -> scale.  Two workgroup
+// barriers (every wave must reach this).  ses = LDS scratch of se_scratch_bytes(F, NB).
+template <int F, int PTN, int NB, int P>
+__device__ __forceinline__ void squeeze_excite(const KParams& kp,
+                                               f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT], int blk,
+                                               float* ses, int co_base, int lane) {
+    using G = Geo<F, PTN, NB, P>;
+    constexpr int CT = G::CT, PT = G::PT;
+    const int g = lane >> 4, li = lane & 15, npos = kp.npos, S = kp.S;
+    float* mean = ses;                 // [NB][F]
+    float* hid = ses + NB * F;         // [NB][kMaxSE]
+    const float inv = 1.f / (float)npos;
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const f32x4 s = board_channel_sum<F, PTN, NB, P>(acc, ct, bb, li, npos);
+            if (li == 0)
+                *(float4*)(mean + bb * F + co_base + 16 * ct + 4 * g) =
+                    make_float4(s[0] * inv, s[1] * inv, s[2] * inv, s[3] * inv);
+        }
+    __syncthreads();
+    const float* w1 = kp.sew1 + (size_t)blk * F * S;
+    for (int i = threadIdx.x; i < NB * S; i += 256) {
+        const int bb = i / S, j = i - bb * S;
+        float h = 0.f;
+        for (int c = 0; c < F; ++c) h += mean[bb * F + c] * w1[c * S + j];
+        hid[bb * kMaxSE + j] = fmaxf(h, 0.f);
+    }
+    __syncthreads();
+    const float* w2 = kp.sew2 + (size_t)blk * S * F;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        const int co = co_base + 16 * ct + 4 * g;
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) {
+            float z0 = 0.f, z1 = 0.f, z2 = 0.f, z3 = 0.f;
+            for (int j = 0; j < S; ++j) {
+                const float h = hid[bb * kMaxSE + j];
+                const float4 w = *(const float4*)(w2 + (size_t)j * F + co);
+                z0 += h * w.x; z1 += h * w.y; z2 += h * w.z; z3 += h * w.w;
+            }
+            const float g0 = 1.f / (1.f + __expf(-z0)), g1 = 1.f / (1.f + __expf(-z1));
+            const float g2 = 1.f / (1.f + __expf(-z2)), g3 = 1.f / (1.f + __expf(-z3));
+#pragma unroll
+            for (int pt = 0; pt < PT; ++pt) {
+                f32x4& v = acc[ct][bb * PT + pt];
+                v[0] *= g0; v[1] *= g1; v[2] *= g2; v[3] *= g3;
+            }
+        }
+    }
+}
+
+// v2 pre-activation of the stream for block blk's first conv: act(s * scale + shift)
+__device__ __forceinline__ f32x4 pre_act(f32x4 v, const float4& sc, const float4& sh, int leaky) {
+    v[0] = act_fn(v[0] * sc.x + sh.x, leaky);
+    v[1] = act_fn(v[1] * sc.y + sh.y, leaky);
+    v[2] = act_fn(v[2] * sc.z + sh.z, leaky);
+    v[3] = act_fn(v[3] * sc.w + sh.w, leaky);
+    return v;
+}
+
+// The trunk of NB boards per workgroup of 4 waves (trunk_kernel / trunk_kernel_v2 below).  V2:
+// pre-activation blocks with optional squeeze-excite (a separate instantiation, so the v1 kernels'
+// register allocation is not burdened by the v2 epilogues).
+template <int F, int PTN, int NB, int WPE, int P, bool V2>
+__device__ __forceinline__ void trunk_body(const KParams& kp) {
     using G = Geo<F, PTN, NB, P>;
     constexpr int P2 = G::P2;
     constexpr int PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, kThreads = 256;
@@ -467,18 +567,21 @@ trunk_kernel(const KParams kp) {
         const float* in = kp.seg[sg].planes + (size_t)(board0 + bb - kp.seg[sg].row0) * C * NPOS;
         for (int i = tid; i < C * NPOS; i += kThreads) sin[i] = live ? in[i] : 0.f;
         __syncthreads();
-        // IM[p][k], k = tap*C + c, zero padded to K0: zero the image, then one thread per
-        // (position, tap) copies its C channels (compile-time divisors only)
+        // IM[p][k], k = tap*C + c (a 1x1 initial conv: k = c), zero padded to K0: zero the image,
+        // then one thread per (position, tap) copies its C channels (compile-time divisors only)
         for (int i = tid; i < P2 * align16((NPOS + 1) * imrow) / 16; i += kThreads) ((uint4*)IM)[i] = uint4{0u, 0u, 0u, 0u};
         __syncthreads();
-        for (int i = tid; i < NPOS * 9; i += kThreads) {
-            const int p = i / 9, tap = i - (i / 9) * 9;
+        const int T0 = kp.k0taps;
+        for (int i = tid; i < NPOS * T0; i += kThreads) {
+            int p = i, tap = 4;                // 1x1: the centre tap only
+            if (T0 == 9) { p = i / 9; tap = i - p * 9; }
             const int r = bd.row(p);
             const int y = r + tap / 3 - 1, x = p - r * W + tap % 3 - 1;
             if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
                 const float* src = sin + y * W + x;
+                const int k0 = T0 == 9 ? tap * C : 0;
                 for (int c = 0; c < C; ++c) {
-                    const int k = tap * C + c;
+                    const int k = k0 + c;
                     const int o = p * imrow + ((((k >> 3) ^ (p & imswz))) << 4) + (k & 7) * 2;
                     const float v = src[c * NPOS];
                     *(__bf16*)(IM + o) = (__bf16)v;
@@ -519,21 +622,31 @@ trunk_kernel(const KParams kp) {
             }
         }
         if constexpr (SI) __syncthreads();    // the image overwrites the im2col scratch
+        // v2: the image feeding block 0 is the pre-activation act(BN_1(s)) of the stream
+        const bool preact = V2 && kp.B > 0;
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
             const float4 bias = *(const float4*)(kp.b0 + co);
+            float4 psc = make_float4(1.f, 1.f, 1.f, 1.f), psh = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (preact) {
+                psc = *(const float4*)(kp.pre + co);
+                psh = *(const float4*)(kp.pre + F + co);
+            }
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) {
                 f32x4 v = acc[ct][bb * PT + pt];
-                v[0] = act_fn(v[0] + bias.x, kp.leaky);
-                v[1] = act_fn(v[1] + bias.y, kp.leaky);
-                v[2] = act_fn(v[2] + bias.z, kp.leaky);
-                v[3] = act_fn(v[3] + bias.w, kp.leaky);
+                v[0] += bias.x; v[1] += bias.y; v[2] += bias.z; v[3] += bias.w;
+                if (!V2 || kp.init_act) {
+                    v[0] = act_fn(v[0], kp.leaky);
+                    v[1] = act_fn(v[1], kp.leaky);
+                    v[2] = act_fn(v[2], kp.leaky);
+                    v[3] = act_fn(v[3], kp.leaky);
+                }
                 if constexpr (RG) rg[(ct * TT + bb * PT + pt) * 64] = v;
                 else resid[ct][bb * PT + pt] = v;
                 acc[ct][bb * PT + pt] = v;    // the heads read acc when there is no residual block
-                store_act<F, PTN, P>(X0 + bb * ACT, 16 * pt + li, co, v, NPOS);
+                store_act<F, PTN, P>(X0 + bb * ACT, 16 * pt + li, co, preact ? pre_act(v, psc, psh, kp.leaky) : v, NPOS);
             }
         }
         __syncthreads();    // scratch is reused by the next board
@@ -556,6 +669,41 @@ trunk_kernel(const KParams kp) {
             // residual tile addresses are formed here, not hoisted out of the loop (44 x 64-bit)
             f32x4* rgc = rg;
             if constexpr (RG) launder_ptr(rgc);
+            if (V2 && second) {   // v2: s += SE(conv2 + bias); image = act(BN_1 of the next block (s))
+                const int blk = cv >> 1;
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) {
+                    const float4 bias = *(const float4*)(bt + co_base + 16 * ct + 4 * g);
+#pragma unroll
+                    for (int t = 0; t < TT; ++t) {
+                        acc[ct][t][0] += bias.x; acc[ct][t][1] += bias.y; acc[ct][t][2] += bias.z; acc[ct][t][3] += bias.w;
+                    }
+                }
+                if (kp.S) squeeze_excite<F, PTN, NB, P>(kp, acc, blk, (float*)(smem + kp.se_off), co_base, lane);
+                const bool more = blk + 1 < kp.B;
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) {
+                    const int co = co_base + 16 * ct + 4 * g;
+                    float4 psc = make_float4(1.f, 1.f, 1.f, 1.f), psh = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (more) {
+                        psc = *(const float4*)(kp.pre + (size_t)(2 * blk + 2) * F + co);
+                        psh = *(const float4*)(kp.pre + (size_t)(2 * blk + 3) * F + co);
+                    }
+#pragma unroll
+                    for (int t = 0; t < TT; ++t) {
+                        f32x4 v = acc[ct][t], r;
+                        if constexpr (RG) r = rgc[(ct * TT + t) * 64];
+                        else r = resid[ct][t];
+                        v[0] += r[0]; v[1] += r[1]; v[2] += r[2]; v[3] += r[3];
+                        if constexpr (RG) rgc[(ct * TT + t) * 64] = v;
+                        else resid[ct][t] = v;
+                        acc[ct][t] = v;
+                        if (more) store_act<F, PTN, P>(X0, 16 * t + li, co, pre_act(v, psc, psh, kp.leaky), NPOS);
+                    }
+                }
+                __syncthreads();
+                continue;
+            }
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
                 const int co = co_base + 16 * ct + 4 * g;
@@ -607,6 +755,38 @@ trunk_kernel(const KParams kp) {
         __syncthreads();
 
         conv3x3<F, PTN, NB, P>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane, bd);
+        if constexpr (V2) {   // s += SE(conv2 + bias); image = act(BN_1 of the next block (s)), model.py:128-149
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const float4 bias = *(const float4*)(b_b + co_base + 16 * ct + 4 * g);
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    acc[ct][t][0] += bias.x; acc[ct][t][1] += bias.y; acc[ct][t][2] += bias.z; acc[ct][t][3] += bias.w;
+                }
+            }
+            if (kp.S) squeeze_excite<F, PTN, NB, P>(kp, acc, blk, (float*)(smem + kp.se_off), co_base, lane);
+            const bool more = blk + 1 < kp.B;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const int co = co_base + 16 * ct + 4 * g;
+                float4 psc = make_float4(1.f, 1.f, 1.f, 1.f), psh = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (more) {
+                    psc = *(const float4*)(kp.pre + (size_t)(2 * blk + 2) * F + co);
+                    psh = *(const float4*)(kp.pre + (size_t)(2 * blk + 3) * F + co);
+                }
+#pragma unroll
+                for (int t = 0; t < TT; ++t) {
+                    f32x4 v = acc[ct][t];
+                    const f32x4 r = resid[ct][t];
+                    v[0] += r[0]; v[1] += r[1]; v[2] += r[2]; v[3] += r[3];
+                    resid[ct][t] = v;
+                    acc[ct][t] = v;
+                    if (more) store_act<F, PTN, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, pre_act(v, psc, psh, kp.leaky), NPOS);
+                }
+            }
+            __syncthreads();
+            continue;
+        }
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -646,6 +826,19 @@ trunk_kernel(const KParams kp) {
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
         const int board = board0 + bb;
+        if (kp.gapF && board < kp.n) {   // pooling value head: the trunk's channel means (model.py:263)
+            const float inv = 1.f / (float)NPOS;
+            float* fo = kp.feat + (size_t)board * kp.FS + 2 * kp.R * NPOS;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const f32x4 sm = board_channel_sum<F, PTN, NB, P>(acc, ct, bb, li, NPOS);
+                const int co = co_base + 16 * ct + 4 * g;
+                if (li == 0)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (co + r < kp.gapF) fo[co + r] = sm[r] * inv;
+            }
+        }
         for (int h = 0; h < HC; ++h) {
             float wv[CT][4];
 #pragma unroll
@@ -668,7 +861,7 @@ trunk_kernel(const KParams kp) {
         }
         __syncthreads();
         if (board < kp.n) {
-            float* fo = kp.feat + (size_t)board * HC * NPOS;
+            float* fo = kp.feat + (size_t)board * kp.FS;
             for (int i = tid; i < HC * NPOS; i += kThreads) {
                 const int h = i / NPOS, p = i - (i / NPOS) * NPOS;
                 float s = kp.bh[h];
@@ -680,7 +873,7 @@ trunk_kernel(const KParams kp) {
                     const int idx = kp.flatten_nchw ? c * NPOS + p : p * 2 + c;
                     fo[r * 2 * NPOS + idx] = s;
                 } else {
-                    fo[2 * kp.R * NPOS + p] = s;
+                    fo[2 * kp.R * NPOS + kp.gapF + p] = s;
                 }
             }
         }
@@ -688,6 +881,20 @@ trunk_kernel(const KParams kp) {
     }
     GZ_STAMP(3);
 #undef GZ_STAMP
+}
+
+// WPE = minimum resident waves per SIMD the register allocation must allow (amdgpu_waves_per_eu),
+// i.e. WPE workgroups per CU.
+template <int F, int PTN, int NB, int WPE, int P>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+trunk_kernel(const KParams kp) {
+    trunk_body<F, PTN, NB, WPE, P, false>(kp);
+}
+
+template <int F, int PTN, int NB, int WPE, int P>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+trunk_kernel_v2(const KParams kp) {
+    trunk_body<F, PTN, NB, WPE, P, true>(kp);
 }
 
 // ---- heads -------------------------------------------------------------------------------------
@@ -700,7 +907,7 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
     constexpr int BPW = kHeadBoards;
     static_assert(BPW == 4, "one float4 of features per k, one softmax wave per board");
     extern __shared__ __attribute__((aligned(16))) float hs[];
-    const int NPOS = kp.npos, HC = 2 * kp.R + 1, FS = HC * NPOS;
+    const int NPOS = kp.npos, FS = kp.FS;
     const int LMAX = kp.maxP > kp.VH ? kp.maxP : kp.VH;
     float* fk = hs;                       // [FS][BPW]
     float* lg = hs + FS * BPW;            // [BPW][LMAX]
@@ -753,14 +960,14 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
         __syncthreads();
     }
 
-    // value head: Dense(HW -> VH) + act, Dense(VH -> V) + softmax
+    // value head: Dense([GAP F] + HW -> VH) + act, Dense(VH -> V) + softmax
     {
-        const int VH = kp.VH;
+        const int VH = kp.VH, VK = kp.gapF + NPOS;
         const float4* f4 = (const float4*)(fk + (size_t)2 * kp.R * NPOS * BPW);
         for (int j = tid; j < VH; j += 256) {
             float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll 8
-            for (int k = 0; k < NPOS; ++k) {
+            for (int k = 0; k < VK; ++k) {
                 const float w = kp.vhw[(size_t)k * VH + j];
                 const float4 f = f4[k];
                 a0 += f.x * w; a1 += f.y * w; a2 += f.z * w; a3 += f.w * w;
@@ -802,8 +1009,8 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
 
 #endif
 
-__host__ inline int heads_lds_bytes(int npos, int R, int maxP, int VH) {
-    const int FS = (2 * R + 1) * npos;
+__host__ inline int heads_lds_bytes(int npos, int R, int maxP, int VH, int gapF) {
+    const int FS = (2 * R + 1) * npos + gapF;
     const int LMAX = maxP > VH ? maxP : VH;
     return (FS * kHeadBoards + kHeadBoards * LMAX + kHeadBoards * 4) * 4;
 }

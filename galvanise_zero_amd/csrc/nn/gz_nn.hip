@@ -45,6 +45,7 @@ struct gz_net {
         int nb = 1;                // boards per workgroup
         int smem = 0;              // dynamic LDS bytes
         int btab_off = 0;          // LDS offset of the bias table
+        int se_off = 0;            // LDS offset of the squeeze-excite scratch
         int resid_bytes = 0;       // global residual scratch per workgroup
     } small, large;                // launches below / from large_min_rows rows
     int large_min_rows = 1 << 30;
@@ -88,9 +89,9 @@ extern "C" const char* gz_nn_last_error(void) { return g_err.c_str(); }
 constexpr int kSmallVariant = 11, kLargeVariant = 21, kLargeMinRows = 257;
 constexpr int kCUs = 256;
 
-static KernelChoice select_kernel(int fpad, int pt, int v, int precision) {
+static KernelChoice select_kernel(int fpad, int pt, int v, int precision, bool v2) {
     if (pt < 1 || pt > kMaxPT) return KernelChoice{};
-    return trunk_variant(fpad, pt, v, precision);
+    return trunk_variant(fpad, pt, v, precision, v2);
 }
 
 // ---- bf16 (round to nearest even) -------------------------------------------------------------
@@ -102,15 +103,24 @@ static inline uint16_t f2bf(float f) {
     return (uint16_t)(u >> 16);
 }
 
+static int initial_kernel(const gz_net_desc& d) {
+    return d.initial_kernel ? d.initial_kernel : (d.resnet_v2 ? 1 : d.cnn_kernel_size);
+}
+static bool has_initial_bn(const gz_net_desc& d) { return !d.resnet_v2 || d.initial_bn; }
+static int gap_features(const gz_net_desc& d) { return d.global_pooling_value ? d.cnn_filter_size : 0; }
+
+// float count of the canonical blob: galvanise_zero_amd/nn/desc.py weight_spec
 static size_t spec_count(const gz_net_desc& d) {
-    const size_t F = d.cnn_filter_size, C = d.input_channels, k = d.cnn_kernel_size;
-    const size_t HW = (size_t)d.input_columns * d.input_rows;
-    size_t n = k * k * C * F + 4 * F;
-    n += (size_t)d.residual_layers * 2 * (k * k * F * F + 4 * F);
-    for (int r = 0; r < d.role_count; ++r) n += F * 2 + 4 * 2 + 2 * HW * d.policy_dist_count[r] + d.policy_dist_count[r];
-    n += F + HW * d.value_hidden_size + d.value_hidden_size + (size_t)d.value_hidden_size * d.num_values + d.num_values;
-    if (d.conv_bias) n += F + (size_t)d.residual_layers * 2 * F + (size_t)d.role_count * 2 + 1;
-    if (d.value_bn) n += 4;
+    const size_t F = d.cnn_filter_size, C = d.input_channels, k = d.cnn_kernel_size, k0 = initial_kernel(d);
+    const size_t HW = (size_t)d.input_columns * d.input_rows, cb = d.conv_bias ? 1 : 0;
+    size_t n = k0 * k0 * C * F + cb * F + (has_initial_bn(d) ? 4 * F : 0);
+    const size_t conv = k * k * F * F + cb * F;
+    const size_t blk = d.resnet_v2 ? 4 * F + conv + 4 * F + conv + 2 * F * (size_t)d.se_units : 2 * (conv + 4 * F);
+    n += (size_t)d.residual_layers * blk;
+    for (int r = 0; r < d.role_count; ++r) n += F * 2 + cb * 2 + 4 * 2 + 2 * HW * d.policy_dist_count[r] + d.policy_dist_count[r];
+    n += F + cb + (d.value_bn ? 4 : 0);
+    n += (gap_features(d) + HW) * d.value_hidden_size + d.value_hidden_size + (size_t)d.value_hidden_size * d.num_values +
+         d.num_values;
     return n;
 }
 
@@ -120,6 +130,11 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     if (d.cnn_kernel_size != 3) { fail("only cnn_kernel_size 3 is supported"); return nullptr; }
     if (d.role_count < 1 || d.role_count > GZ_MAX_ROLES) { fail("role_count out of range"); return nullptr; }
     if (d.num_values < 1 || d.num_values > 4) { fail("num_values out of range"); return nullptr; }
+    if (initial_kernel(d) != 1 && initial_kernel(d) != 3) { fail("initial conv kernel must be 1 or 3"); return nullptr; }
+    if (d.se_units < 0 || d.se_units > kMaxSE || (d.se_units && !d.resnet_v2)) {
+        fail("squeeze-excite units must be 0.." + std::to_string(kMaxSE) + " on a v2 net");
+        return nullptr;
+    }
     const int precision = d.precision == 0 ? GZ_PRECISION_BF16 : d.precision;
     if (precision != GZ_PRECISION_BF16 && precision != GZ_PRECISION_SPLIT) { fail("unknown precision"); return nullptr; }
     int vs = kSmallVariant, vl = kLargeVariant, min_large = kLargeMinRows;
@@ -133,8 +148,9 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     const int npos_ = d.input_columns * d.input_rows;
     const int pt = (npos_ + 15) / 16;
     if (d.input_rows > 32 || npos_ >= 1024) { fail("board too large"); return nullptr; }
-    const KernelChoice kc = select_kernel(fpad, pt, vs, precision);
-    KernelChoice kl = select_kernel(fpad, pt, vl, precision);
+    const bool v2 = d.resnet_v2 != 0;
+    const KernelChoice kc = select_kernel(fpad, pt, vs, precision, v2);
+    KernelChoice kl = select_kernel(fpad, pt, vl, precision, v2);
     if (kc.fn && !kl.fn && vl != vs) {   // geometries with a single (one board per workgroup) variant
         kl = kc;
         min_large = 1 << 30;
@@ -142,7 +158,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     if (!kc.fn || !kl.fn) {
         fail("unsupported network geometry F=" + std::to_string(d.cnn_filter_size) + " H=" +
              std::to_string(d.input_columns) + " W=" + std::to_string(d.input_rows) +
-             (precision == GZ_PRECISION_SPLIT ? " (split precision)" : ""));
+             (precision == GZ_PRECISION_SPLIT ? " (split precision)" : "") + (v2 ? " (v2 nets: F <= 128)" : ""));
         return nullptr;
     }
     gz_net* net = new gz_net;
@@ -151,7 +167,8 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     net->large_min_rows = min_large;
     net->p2 = precision == GZ_PRECISION_SPLIT ? 2 : 1;
     net->fpad = fpad;
-    net->K0 = ((9 * d.input_channels + 31) / 32) * 32;
+    const int k0 = initial_kernel(d);
+    net->K0 = ((k0 * k0 * d.input_channels + 31) / 32) * 32;
     net->nweights = spec_count(d);
     int maxP = 0;
     for (int r = 0; r < d.role_count; ++r) maxP = std::max(maxP, d.policy_dist_count[r]);
@@ -167,11 +184,13 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
                                     : c.nb * c.act_bytes + std::max(c.nb * c.act_bytes, scr);
         t.resid_bytes = c.resid_bytes;
         t.smem = t.btab_off + bias_table_bytes(fpad, d.residual_layers);
+        t.se_off = t.smem;
+        if (d.se_units) t.smem += se_scratch_bytes(fpad, c.nb);
         return t;
     };
     net->small = trunk(kc);
     net->large = trunk(kl);
-    net->heads_smem = heads_lds_bytes(npos, d.role_count, maxP, d.value_hidden_size);
+    net->heads_smem = heads_lds_bytes(npos, d.role_count, maxP, d.value_hidden_size, gap_features(d));
     KParams& kp = net->kp;
     kp.C = d.input_channels;
     kp.K0 = net->K0;
@@ -182,6 +201,12 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     kp.leaky = d.leaky_relu;
     kp.flatten_nchw = d.flatten_nchw;
     kp.value_sigmoid = d.value_sigmoid;
+    kp.v2 = d.resnet_v2 ? 1 : 0;
+    kp.k0taps = k0 * k0;
+    kp.init_act = has_initial_bn(d) ? 1 : 0;
+    kp.S = d.se_units;
+    kp.gapF = gap_features(d);
+    kp.FS = (2 * d.role_count + 1) * npos + kp.gapF;
     kp.maxP = maxP;
     kp.npos = npos;
     kp.H = d.input_columns;
@@ -235,11 +260,13 @@ extern "C" void gz_net_destroy(gz_net* net) {
 extern "C" size_t gz_net_weight_count(const gz_net* net) { return net ? net->nweights : 0; }
 
 extern "C" double gz_net_flops_per_eval(const gz_net* net) {
-    const gz_net_desc& d = net->d;
+    const gz_net_desc& d = net->d;   // = NetDesc.flops_per_eval (desc.py)
     const double F = d.cnn_filter_size, C = d.input_channels, HW = (double)d.input_columns * d.input_rows;
-    double f = 2 * HW * C * F * 9 + d.residual_layers * 2 * (2 * HW * F * F * 9);
+    const double k0 = initial_kernel(d);
+    double f = 2 * HW * C * F * k0 * k0 + d.residual_layers * 2 * (2 * HW * F * F * 9);
+    f += d.residual_layers * 2.0 * (2 * F * d.se_units);
     for (int r = 0; r < d.role_count; ++r) f += 2 * HW * F * 2 + 2 * (2 * HW) * d.policy_dist_count[r];
-    f += 2 * HW * F + 2 * HW * d.value_hidden_size + 2.0 * d.value_hidden_size * d.num_values;
+    f += 2 * HW * F + 2 * (gap_features(d) + HW) * d.value_hidden_size + 2.0 * d.value_hidden_size * d.num_values;
     return f;
 }
 
@@ -302,13 +329,20 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     };
     auto conv_bias = [&](int n) -> const float* { return d.conv_bias ? cur.take(n) : nullptr; };
     std::vector<float> s, bb;
-    {   // initial conv [3][3][C][F] -> w0[kc][co][32], k = tap*C + c
-        const float* w = cur.take((size_t)9 * C * F);
+    const int k0 = initial_kernel(d), T0 = k0 * k0, S = d.se_units;
+    {   // initial conv [k0][k0][C][F] -> w0[kc][co][32], k = tap*C + c
+        const float* w = cur.take((size_t)T0 * C * F);
         const float* cb = conv_bias(F);
-        bn_fold(F, s, bb, cb);
+        if (has_initial_bn(d)) {
+            bn_fold(F, s, bb, cb);
+        } else {   // v2 files with a bare initial conv: s = conv (+ bias), no BN, no activation
+            s.assign(F, 1.f);
+            bb.assign(F, 0.f);
+            if (cb) for (int i = 0; i < F; ++i) bb[i] = cb[i];
+        }
         for (int co = 0; co < F; ++co) {
             b0[co] = bb[co];
-            for (int k = 0; k < 9 * C; ++k) {
+            for (int k = 0; k < T0 * C; ++k) {
                 const int tap = k / C, c = k % C;
                 const float v = w[((size_t)tap * C + c) * F + co] * s[co];
                 w0[((size_t)(k / 32) * FP + co) * 32 + (k % 32)] = f2bf(v);
@@ -316,21 +350,56 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
             }
         }
     }
-    // [3][3][F][F] -> [tap][kc][co][32] (split precision: [tap][kc][co][hi 32 | lo 32])
-    for (int conv = 0; conv < 2 * B; ++conv) {
-        const float* w = cur.take((size_t)9 * F * F);
-        const float* cb = conv_bias(F);
-        bn_fold(F, s, bb, cb);
+    // trunk conv `conv` [3][3][F][F] * scale[co] -> [tap][kc][co][32] (split precision:
+    // [tap][kc][co][hi 32 | lo 32]), bias[co] -> bres
+    auto pack_conv = [&](int conv, const float* w, const std::vector<float>& scale, const std::vector<float>& bias) {
         uint16_t* dst = wres.data() + (size_t)P2 * conv * 9 * FP * FP;
         for (int co = 0; co < F; ++co) {
-            bres[(size_t)conv * FP + co] = bb[co];
+            bres[(size_t)conv * FP + co] = bias[co];
             for (int tap = 0; tap < 9; ++tap)
                 for (int ci = 0; ci < F; ++ci) {
-                    const float v = w[((size_t)tap * F + ci) * F + co] * s[co];
+                    const float v = w[((size_t)tap * F + ci) * F + co] * scale[co];
                     const size_t o = ((((size_t)tap * KC + ci / 32) * FP + co) * P2) * 32 + (ci % 32);
                     dst[o] = f2bf(v);
                     if (P2 == 2) dst[o + 32] = lo_of(v);
                 }
+        }
+    };
+    std::vector<float> pre(d.resnet_v2 ? (size_t)2 * B * FP : 1, 0.f);
+    std::vector<float> sew1(S ? (size_t)B * FP * S : 1, 0.f), sew2(S ? (size_t)B * S * FP : 1, 0.f);
+    for (int blk = 0; blk < B; ++blk) {
+        if (!d.resnet_v2) {      // conv-BN-act-conv-BN-add-act: both BNs fold into their convs
+            for (int j = 0; j < 2; ++j) {
+                const float* w = cur.take((size_t)9 * F * F);
+                const float* cb = conv_bias(F);
+                bn_fold(F, s, bb, cb);
+                pack_conv(2 * blk + j, w, s, bb);
+            }
+            continue;
+        }
+        // v2: BN_1 (scale / shift applied to the stream when the block's input image is written),
+        // conv1 with BN_2 folded, conv2 (no BN), squeeze-excite dense layers
+        bn_fold(F, s, bb);
+        for (int co = 0; co < F; ++co) {
+            pre[(size_t)(2 * blk) * FP + co] = s[co];
+            pre[(size_t)(2 * blk + 1) * FP + co] = bb[co];
+        }
+        const float* w1 = cur.take((size_t)9 * F * F);
+        const float* cb1 = conv_bias(F);
+        bn_fold(F, s, bb, cb1);
+        pack_conv(2 * blk, w1, s, bb);
+        const float* w2 = cur.take((size_t)9 * F * F);
+        const float* cb2 = conv_bias(F);
+        std::vector<float> one(F, 1.f), b2(F, 0.f);
+        if (cb2) for (int co = 0; co < F; ++co) b2[co] = cb2[co];
+        pack_conv(2 * blk + 1, w2, one, b2);
+        if (S) {
+            const float* c = cur.take((size_t)F * S);   // Dense [F][S]
+            const float* gt = cur.take((size_t)S * F);  // Dense [S][F]
+            for (int ci = 0; ci < F; ++ci)
+                for (int j = 0; j < S; ++j) sew1[((size_t)blk * FP + ci) * S + j] = c[(size_t)ci * S + j];
+            for (int j = 0; j < S; ++j)
+                for (int co = 0; co < F; ++co) sew2[((size_t)blk * S + j) * FP + co] = gt[(size_t)j * F + co];
         }
     }
     std::vector<const float*> pdense(R), pbias(R);
@@ -357,7 +426,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
         for (int f = 0; f < F; ++f) wh[(size_t)(2 * R) * FP + f] = w[f] * vs;
         bh[2 * R] = vb;
     }
-    const float* vhw = cur.take((size_t)HW * d.value_hidden_size);
+    const int VK = gap_features(d) + HW;     // value hidden inputs: [GAP F] + HW
+    const float* vhw = cur.take((size_t)VK * d.value_hidden_size);
     const float* vhb = cur.take(d.value_hidden_size);
     const float* vdw = cur.take((size_t)d.value_hidden_size * d.num_values);
     const float* vdb = cur.take(d.num_values);
@@ -374,7 +444,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
         o_pd[r] = L.alloc((size_t)2 * HW * d.policy_dist_count[r] * 4);
         o_pb[r] = L.alloc((size_t)d.policy_dist_count[r] * 4);
     }
-    const size_t o_vhw = L.alloc((size_t)HW * d.value_hidden_size * 4), o_vhb = L.alloc(d.value_hidden_size * 4);
+    const size_t o_vhw = L.alloc((size_t)VK * d.value_hidden_size * 4), o_vhb = L.alloc(d.value_hidden_size * 4);
+    const size_t o_pre = L.alloc(pre.size() * 4), o_sew1 = L.alloc(sew1.size() * 4), o_sew2 = L.alloc(sew2.size() * 4);
     const size_t o_vdw = L.alloc((size_t)d.value_hidden_size * d.num_values * 4), o_vdb = L.alloc(d.num_values * 4);
 
     std::vector<char> img(L.off, 0);
@@ -391,7 +462,10 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
         put(o_pd[r], pdense[r], (size_t)2 * HW * d.policy_dist_count[r] * 4);
         put(o_pb[r], pbias[r], (size_t)d.policy_dist_count[r] * 4);
     }
-    put(o_vhw, vhw, (size_t)HW * d.value_hidden_size * 4);   // Keras layout [HW][VH]
+    put(o_vhw, vhw, (size_t)VK * d.value_hidden_size * 4);   // Keras layout [VK][VH]
+    put(o_pre, pre.data(), pre.size() * 4);
+    put(o_sew1, sew1.data(), sew1.size() * 4);
+    put(o_sew2, sew2.data(), sew2.size() * 4);
     put(o_vhb, vhb, d.value_hidden_size * 4);
     put(o_vdw, vdw, (size_t)d.value_hidden_size * d.num_values * 4);
     put(o_vdb, vdb, d.num_values * 4);
@@ -424,6 +498,9 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     kp.vhb = (const float*)(m + o_vhb);
     kp.vdw = (const float*)(m + o_vdw);
     kp.vdb = (const float*)(m + o_vdb);
+    kp.pre = (const float*)(m + o_pre);
+    kp.sew1 = (const float*)(m + o_sew1);
+    kp.sew2 = (const float*)(m + o_sew2);
     net->has_weights = true;
     wl.unlock();
     if (old) {   // launches already queued may still read the old image
@@ -473,7 +550,7 @@ static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* se
                 f.first = nullptr;
             }
             const int cap = std::max(n, 8192);
-            HIPCHK(hipMalloc((void**)&f.first, (size_t)cap * (2 * kp.R + 1) * kp.npos * sizeof(float)));
+            HIPCHK(hipMalloc((void**)&f.first, (size_t)cap * kp.FS * sizeof(float)));
             f.second = cap;
         }
         kp.feat = f.first;
@@ -497,6 +574,7 @@ static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* se
         kp.resid = (f32x4*)f.first;
     }
     kp.btab_off = t.btab_off;
+    kp.se_off = t.se_off;
     void* args[] = {&kp};
     HIPCHK(hipLaunchKernel(t.fn, dim3((n + t.nb - 1) / t.nb), dim3(256), args, t.smem, stream));
     if (mid) HIPCHK(hipEventRecord(mid, stream));

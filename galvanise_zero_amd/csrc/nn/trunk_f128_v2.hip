@@ -1,0 +1,22 @@
+// Trunk kernels with 128 filters, v2 (pre-activation / squeeze-excite) nets (trunk_variants.h).
+#include "trunk_variants.h"
+
+namespace gznn {
+
+KernelChoice trunk_variant_f128_v2(int pt, int v, int precision) {
+    switch (pt) {
+        case 2: return variants<128, 2, true>(v, precision);
+        case 3: return variants<128, 3, true>(v, precision);
+        case 4: return variants<128, 4, true>(v, precision);
+        case 5: return variants<128, 5, true>(v, precision);
+        case 6: return variants<128, 6, true>(v, precision);
+        case 7: return variants<128, 7, true>(v, precision);
+        case 8: return variants<128, 8, true>(v, precision);
+        case 9: return variants<128, 9, true>(v, precision);
+        case 10: return variants<128, 10, true>(v, precision);
+        case 11: return variants<128, 11, true>(v, precision);
+        default: return KernelChoice{};
+    }
+}
+
+}  // namespace gznn

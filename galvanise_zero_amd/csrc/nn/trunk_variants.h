@@ -5,7 +5,9 @@
 // other filter counts with zero channels), PT = position tiles of 16 (boards of up to 16 * PT
 // positions, H and W given at run time).  Variants per geometry: NB boards per workgroup x WPE
 // workgroups per CU ("11", "12", "21"), and the split-precision kernel (P = 3, one board per
-// workgroup, boards of up to 64 positions).
+// workgroup, boards of up to 64 positions).  v2 (pre-activation / squeeze-excite) nets use the
+// trunk_kernel_v2 instantiations of the same variants (trunk_f64_v2.hip, trunk_f128_v2.hip; the
+// reference's v2 nets have at most 128 filters).
 #pragma once
 
 #include "forward_kernel.h"
@@ -20,10 +22,11 @@ struct KernelChoice {
     int resid_bytes = 0;           // global residual scratch per workgroup (0: registers)
 };
 
-template <int F, int PTN, int NB, int WPE, int P = 1>
+template <int F, int PTN, int NB, int WPE, int P = 1, bool V2 = false>
 KernelChoice kernel_for() {
     KernelChoice k;
-    k.fn = (const void*)&trunk_kernel<F, PTN, NB, WPE, P>;
+    if constexpr (V2) k.fn = (const void*)&trunk_kernel_v2<F, PTN, NB, WPE, P>;
+    else k.fn = (const void*)&trunk_kernel<F, PTN, NB, WPE, P>;
     k.act_bytes = Geo<F, PTN, NB, P>::ACT_BYTES;
     k.nb = NB;
     k.single_image = Geo<F, PTN, NB, P>::SI;
@@ -32,27 +35,27 @@ KernelChoice kernel_for() {
 }
 
 // precision 3: split (hi / lo) operands; otherwise bf16.  v = NB * 10 + WPE.
-template <int F, int PTN>
+template <int F, int PTN, bool V2 = false>
 KernelChoice variants(int v, int precision) {
     if (precision == 3) {
         if constexpr (F <= 128 && PTN <= 4) {
             if constexpr (2 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024) {
-                if (v == 11) return kernel_for<F, PTN, 1, 1, 3>();
+                if (v == 11) return kernel_for<F, PTN, 1, 1, 3, V2>();
                 // two boards per workgroup (F = 128: 256-byte wrapped rows, hi + lo in 512 bytes)
                 if constexpr (Geo<F, PTN, 1, 3>::WRAP && 4 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024)
-                    if (v == 21) return kernel_for<F, PTN, 2, 1, 3>();
+                    if (v == 21) return kernel_for<F, PTN, 2, 1, 3, V2>();
             }
         }
         return KernelChoice{};
     }
     if constexpr (4 * Geo<F, PTN, 1>::ACT_BYTES + 16 * 1024 > 160 * 1024) {   // one board per workgroup only
-        return v == 11 ? kernel_for<F, PTN, 1, 1>() : KernelChoice{};
+        return v == 11 ? kernel_for<F, PTN, 1, 1, 1, V2>() : KernelChoice{};
     } else {
         switch (v) {
-            case 11: return kernel_for<F, PTN, 1, 1>();
-            case 12: if constexpr (PTN == 4) return kernel_for<F, PTN, 1, 2>(); else return KernelChoice{};
+            case 11: return kernel_for<F, PTN, 1, 1, 1, V2>();
+            case 12: if constexpr (PTN == 4) return kernel_for<F, PTN, 1, 2, 1, V2>(); else return KernelChoice{};
             case 21:   // (not where the two boards' tiles would spill registers)
-                if constexpr (Geo<F, PTN, 2>::LIVE_VGPRS <= 300) return kernel_for<F, PTN, 2, 1>();
+                if constexpr (Geo<F, PTN, 2>::LIVE_VGPRS <= 300) return kernel_for<F, PTN, 2, 1, 1, V2>();
                 else return KernelChoice{};
             default: return KernelChoice{};
         }
@@ -62,12 +65,19 @@ KernelChoice variants(int v, int precision) {
 KernelChoice trunk_variant_f64(int pt, int v, int precision);
 KernelChoice trunk_variant_f128(int pt, int v, int precision);
 KernelChoice trunk_variant_f256(int pt, int v, int precision);
+KernelChoice trunk_variant_f64_v2(int pt, int v, int precision);
+KernelChoice trunk_variant_f128_v2(int pt, int v, int precision);
 
 // padded filter count and position tiles of a board; 0 when not compiled
 inline int padded_filters(int F) { return F <= 64 ? 64 : F <= 128 ? 128 : F <= 256 ? 256 : 0; }
 constexpr int kMaxPT = 11;   // boards of up to 176 positions (13 x 13)
 
-inline KernelChoice trunk_variant(int fpad, int pt, int v, int precision) {
+inline KernelChoice trunk_variant(int fpad, int pt, int v, int precision, bool v2 = false) {
+    if (v2) {
+        if (fpad == 64) return trunk_variant_f64_v2(pt, v, precision);
+        if (fpad == 128) return trunk_variant_f128_v2(pt, v, precision);
+        return KernelChoice{};
+    }
     if (fpad == 64) return trunk_variant_f64(pt, v, precision);
     if (fpad == 128) return trunk_variant_f128(pt, v, precision);
     if (fpad == 256) return trunk_variant_f256(pt, v, precision);

@@ -1,13 +1,28 @@
-"""Network description + canonical weight-blob layout for the v1 (AlphaGo-Zero style) residual CNN.
+"""Network description + canonical weight-blob layout of the residual policy/value CNN.
 
-Restates the topology built by ``get_network_model`` (reference ``src/ggpzero/nn/model.py:154-296``)
-for the ``resnet_v2=False`` path, which is the one every BASELINE config uses:
+Restates the topologies built by ``get_network_model`` (reference ``src/ggpzero/nn/model.py:154-296``).
+v1 (``resnet_v2=False``, AlphaGo-Zero style; every BASELINE config):
 
 * initial ``conv2d_block(F, k, use_bias=False) -> BN -> act``            (model.py:205-208, 25-44)
 * ``residual_layers`` x ``residual_block_v1``: conv-BN-act-conv-BN-add-act (model.py:47-75)
+
+v2 (``resnet_v2=True``, pre-activation; the reference's ``features=True`` templates and its non-legacy
+model files, e.g. data/breakthroughSmall/models/b1_58.json):
+
+* initial ``conv2d_block(F, 1)`` -> BN -> act (model.py:176-179); older model files have a bare 1x1
+  conv there (``initial_bn=False``: no BN, no activation)
+* ``residual_layers`` x ``residual_block_v2(num_convs=2)``: BN-act-conv-BN-act-conv, optional
+  squeeze-excite gate (GlobalAveragePooling -> Dense(S, relu, no bias) -> Dense(F, sigmoid, no bias)
+  -> multiply), add -- no activation after the add (model.py:78-151); dropout is inference-identity
+* the heads read the last add directly (no final BN / activation)
+
+Heads (both):
+
 * per role: ``conv2d_block(2, 1)`` -> BN -> act -> Flatten -> Dense(P_r, softmax)  (model.py:223-241)
 * value:  ``conv2d_block(1, 1, do_bn=False)`` -> act -> Flatten -> Dense(hidden, act)
-  -> Dense(V, softmax)                                                     (model.py:273-291)
+  -> Dense(V, softmax)                                                     (model.py:273-291);
+  with ``global_pooling_value`` the value 1x1 conv has BN and the flat features are
+  [GlobalAveragePooling(trunk) (F), conv (HW)] concatenated in that order (model.py:262-271)
 
 BatchNormalization is inference-mode with epsilon 1e-3 (Keras default; every
 ``data/*/models/*.json`` records ``epsilon: 0.001``).
@@ -49,6 +64,25 @@ class NetDesc:
     conv_bias: bool = False
     value_bn: bool = False
     value_sigmoid: bool = False
+    # v2 (pre-activation) trunk, model.py:78-151, 171-198
+    resnet_v2: bool = False
+    initial_bn: bool = True          # v2 initial 1x1 conv followed by BN + act (False: bare conv)
+    se_units: int = 0                # squeeze-excite compress units (0: no SE; model.py: F // 3)
+    global_pooling_value: bool = False
+    # initial conv kernel: 0 = model.py's (1 for v2, cnn_kernel_size for v1); some v2 model files
+    # (e.g. data/hexLG13/models/b4_305.json) have a 3x3 initial conv + BN + act
+    initial_kernel_size: int = 0
+
+    @property
+    def initial_kernel(self):
+        if self.initial_kernel_size:
+            return self.initial_kernel_size
+        return 1 if self.resnet_v2 else self.cnn_kernel_size
+
+    @property
+    def value_features(self):
+        """Inputs of the value hidden Dense: [GAP (F)] + the value conv's HW."""
+        return (self.cnn_filter_size if self.global_pooling_value else 0) + self.hw
 
     @property
     def role_count(self):
@@ -60,19 +94,18 @@ class NetDesc:
 
     def flops_per_eval(self):
         """Algorithmic FLOPs (2/MAC) of one leaf evaluation, BN/act/softmax excluded."""
-        F, C, HW, k = self.cnn_filter_size, self.input_channels, self.hw, self.cnn_kernel_size
-        f = 2 * HW * C * F * k * k
-        f += self.residual_layers * 2 * (2 * HW * F * F * k * k)
+        f = self.flops_trunk()
         for p in self.policy_dist_count:
-            f += 2 * HW * F * 2 + 2 * (2 * HW) * p
-        f += 2 * HW * F + 2 * HW * self.value_hidden_size + 2 * self.value_hidden_size * self.num_values
+            f += 2 * (2 * self.hw) * p
+        f += 2 * self.value_features * self.value_hidden_size + 2 * self.value_hidden_size * self.num_values
         return f
 
-
     def flops_trunk(self):
-        """FLOPs of the trunk kernel per evaluation: every conv incl. the heads' 1x1 convs."""
-        F, C, HW, k = self.cnn_filter_size, self.input_channels, self.hw, self.cnn_kernel_size
-        f = 2 * HW * C * F * k * k + self.residual_layers * 2 * (2 * HW * F * F * k * k)
+        """FLOPs of the trunk kernel per evaluation: every conv incl. the heads' 1x1 convs, and the
+        squeeze-excite dense layers."""
+        F, C, HW, k, k0 = self.cnn_filter_size, self.input_channels, self.hw, self.cnn_kernel_size, self.initial_kernel
+        f = 2 * HW * C * F * k0 * k0 + self.residual_layers * 2 * (2 * HW * F * F * k * k)
+        f += self.residual_layers * 2 * (2 * F * self.se_units)
         return f + (2 * self.role_count + 1) * 2 * HW * F
 
     def flops_heads(self):
@@ -94,13 +127,24 @@ def weight_spec(d: NetDesc) -> List[Tuple[str, Tuple[int, ...]]]:
         if d.conv_bias:                     # Keras Conv2D weights: [kernel, bias]
             spec.append((name + "_bias", (shape[3],)))
 
-    conv("initial_conv", (k, k, C, F))
-    bn("initial_bn", F)
+    k0 = d.initial_kernel
+    conv("initial_conv", (k0, k0, C, F))
+    if d.initial_bn or not d.resnet_v2:
+        bn("initial_bn", F)
     for i in range(d.residual_layers):
-        conv("res%d_conv0" % i, (k, k, F, F))
-        bn("res%d_bn0" % i, F)
-        conv("res%d_conv1" % i, (k, k, F, F))
-        bn("res%d_bn1" % i, F)
+        if d.resnet_v2:                      # BN-act-conv-BN-act-conv [SE] add   (model.py:128-149)
+            bn("res%d_bn1" % i, F)
+            conv("res%d_conv1" % i, (k, k, F, F))
+            bn("res%d_bn2" % i, F)
+            conv("res%d_conv2" % i, (k, k, F, F))
+            if d.se_units:
+                spec.append(("res%d_se_compress" % i, (F, d.se_units)))
+                spec.append(("res%d_se_gating" % i, (d.se_units, F)))
+        else:
+            conv("res%d_conv0" % i, (k, k, F, F))
+            bn("res%d_bn0" % i, F)
+            conv("res%d_conv1" % i, (k, k, F, F))
+            bn("res%d_bn1" % i, F)
     for r, p in enumerate(d.policy_dist_count):
         conv("policy%d_conv" % r, (1, 1, F, 2))
         bn("policy%d_bn" % r, 2)
@@ -109,7 +153,7 @@ def weight_spec(d: NetDesc) -> List[Tuple[str, Tuple[int, ...]]]:
     conv("value_conv", (1, 1, F, 1))
     if d.value_bn:
         bn("value_bn", 1)
-    spec.append(("value_hidden", (d.hw, d.value_hidden_size)))
+    spec.append(("value_hidden", (d.value_features, d.value_hidden_size)))
     spec.append(("value_hidden_bias", (d.value_hidden_size,)))
     spec.append(("value_dense", (d.value_hidden_size, d.num_values)))
     spec.append(("value_bias", (d.num_values,)))

@@ -2,9 +2,8 @@
 
 ``desc_from_keras_json`` reads a ``data/<game>/models/<gen>.json`` document (the Keras
 ``model.to_json()`` the reference's manager writes, ``manager.py:113-127``) and returns the
-:class:`NetDesc` of a v1 (AlphaGo-Zero style) residual net, the topology ``get_network_model``
-builds with ``resnet_v2=False`` (``model.py:154-296``) and the one the fused forward implements.  Both
-generations of v1 files are recognised:
+:class:`NetDesc` of the residual net ``get_network_model`` builds (``model.py:154-296``), v1 or v2.
+Both generations of v1 files are recognised:
 
 * current ``model.py`` naming: ``initial-conv_conv2d`` / ``_bn``, ``ResLayer_<i>_conv0..bn1``,
   ``to_flatten_policy_head_<r>_conv2d`` / ``_bn``, ``value_flatten_conv2d`` (no BN), ``value_hidden``,
@@ -13,8 +12,13 @@ generations of v1 files are recognised:
   bias, ``to_flatten_value_head_conv2d`` + ``_bn``, ``value_hidden_layer``, sigmoid ``value`` -> the
   ``conv_bias`` / ``value_bn`` / ``value_sigmoid`` flags.
 
-v2 / squeeze-excitation / global-average-pool nets (``model.py:78-151, 251-271``) raise
-:class:`NotSupported`: none of the BASELINE configs uses them.
+v2 files (``model.py:78-151``): ``ResLayer_<i>_bn_1 / conv1 / bn_2 / conv2`` pre-activation blocks,
+optional ``ResLayer_<i>_se_compress / se_gating`` squeeze-excite Dense layers, a 1x1 ``initial-conv``
+(bare in older files, ``initial-conv_conv2d / _bn`` in current ones) and the global-pooling value head
+(``value_average`` + ``value_flatten_conv2d`` [+ ``_bn``], concatenated GAP-first, ``model.py:262-271``).
+Files built by older model.py revisions with layers the current one cannot produce
+(AveragePooling2D / Lambda reward heads, e.g. ``hexLG13/models/h1_229.json``) and the
+``concat_all_layers`` value head raise :class:`NotSupported`.
 
 ``weights_from_keras`` maps per-layer Keras weight lists (``layer.get_weights()``: Conv2D
 ``[kernel HWIO, bias?]``, BatchNormalization ``[gamma, beta, moving_mean, moving_variance]``, Dense
@@ -28,12 +32,8 @@ import numpy as np
 
 from .desc import NetDesc, weight_spec
 
-UNSUPPORTED_LAYERS = {"GlobalAveragePooling2D": "global-average-pool / squeeze-excitation (model.py:100-126, 263)",
-                      "Multiply": "squeeze-excitation gating (model.py:126)",
-                      "AveragePooling2D": "pooled value head",
-                      "Concatenate": "concatenated value head (model.py:263-271)",
-                      "Lambda": "custom Lambda layer",
-                      "Permute": "squeeze-excitation permute (model.py:125)"}
+UNSUPPORTED_LAYERS = {"AveragePooling2D": "pooled reward head (not produced by model.py:154-296)",
+                      "Lambda": "custom Lambda layer"}
 
 
 class NotSupported(Exception):
@@ -53,17 +53,22 @@ def _inbound(layer):
 
 
 def _is_conv(role):
-    return re.match(r"(initial_conv|res\d+_conv[01]|policy\d+_conv|value_conv)$", role) is not None
+    return re.match(r"(initial_conv|res\d+_conv[012]|policy\d+_conv|value_conv)$", role) is not None
 
 
 def _is_bn(role):
-    return re.match(r"(initial_bn|res\d+_bn[01]|policy\d+_bn|value_bn)$", role) is not None
+    return re.match(r"(initial_bn|res\d+_bn[012]|policy\d+_bn|value_bn)$", role) is not None
+
+
+def _is_se(role):
+    return re.match(r"res\d+_se_(compress|gating)$", role) is not None
 
 
 def roles(doc):
-    """Maps every weight-carrying layer name of a v1 model file to its role in weight_spec:
-    ('initial_conv' | 'res<i>_conv<j>' | 'policy<r>_conv' | 'value_conv' | <same>_bn | 'policy<r>_dense'
-    | 'value_hidden' | 'value_dense')."""
+    """Maps every weight-carrying layer name of a model file to its role in weight_spec:
+    ('initial_conv' | 'res<i>_conv<j>' | 'policy<r>_conv' | 'value_conv' | <same>_bn | 'res<i>_bn<j>'
+    (v2 pre-activation) | 'res<i>_se_compress' | 'res<i>_se_gating' | 'policy<r>_dense' | 'value_hidden'
+    | 'value_dense')."""
     doc, layers = _layers(doc)
     by_name = {l["name"]: l for l in layers}
     out = {}
@@ -71,7 +76,7 @@ def roles(doc):
     for l in layers:
         n, cls = l["name"], l["class_name"]
         if cls == "Conv2D":
-            m = re.match(r"ResLayer_(\d+)_conv([01])$", n)
+            m = re.match(r"ResLayer_(\d+)_conv([012])$", n)
             if m:
                 out[n] = "res%s_conv%s" % m.groups()
             elif _inbound(l) == inp:
@@ -90,10 +95,17 @@ def roles(doc):
                 out[n] = "value_hidden"
             elif n == "value":
                 out[n] = "value_dense"
+            elif re.match(r"ResLayer_(\d+)_se_(compress|gating)$", n):
+                i, kind = re.match(r"ResLayer_(\d+)_se_(compress|gating)$", n).groups()
+                out[n] = "res%s_se_%s" % (i, kind)
             else:
                 raise NotSupported("unrecognised Dense %s" % n)
     for l in layers:
         if l["class_name"] == "BatchNormalization":
+            m = re.match(r"ResLayer_(\d+)_bn_([12])$", l["name"])
+            if m:                   # v2 pre-activation BN (its input is the stream or conv1)
+                out[l["name"]] = "res%s_bn%s" % m.groups()
+                continue
             src = _inbound(l)
             if len(src) != 1 or src[0] not in out or by_name[src[0]]["class_name"] != "Conv2D":
                 raise NotSupported("BatchNormalization %s not after a conv" % l["name"])
@@ -102,7 +114,7 @@ def roles(doc):
 
 
 def desc_from_keras_json(doc):
-    """NetDesc of a v1 model file; NotSupported for other topologies."""
+    """NetDesc of a v1 or v2 model file; NotSupported for other topologies."""
     doc, layers = _layers(doc)
     for l in layers:
         if l["class_name"] in UNSUPPORTED_LAYERS:
@@ -110,6 +122,7 @@ def desc_from_keras_json(doc):
     r = roles(doc)
     cfg = {l["name"]: l["config"] for l in layers}
     cls = {l["name"]: l["class_name"] for l in layers}
+    by_name = {l["name"]: l for l in layers}
     inp = next(l for l in layers if l["class_name"] == "InputLayer")
     shape = inp["config"]["batch_input_shape"]
     conv0 = next(n for n, v in r.items() if v == "initial_conv")
@@ -117,7 +130,13 @@ def desc_from_keras_json(doc):
         raise NotSupported("channels_last input")
     C, H, W = shape[1], shape[2], shape[3]
     F = cfg[conv0]["filters"]
-    k = cfg[conv0]["kernel_size"][0]
+    v2 = any(re.match(r"ResLayer_\d+_(bn_[12]|conv2)$", n) for n in r)
+    res_convs = [n for n, v in r.items() if re.match(r"res\d+_conv", v)]
+    k = cfg[res_convs[0]]["kernel_size"][0] if res_convs else cfg[conv0]["kernel_size"][0]
+    k0 = cfg[conv0]["kernel_size"][0]
+    if k0 not in (1, 3) or cfg[conv0]["kernel_size"][1] != k0:
+        raise NotSupported("initial conv kernel %s" % (cfg[conv0]["kernel_size"],))
+    default_k0 = 1 if v2 else k
     blocks = sorted({int(v[3:v.index("_")]) for v in r.values() if v.startswith("res")})
     if blocks != list(range(len(blocks))):
         raise NotSupported("residual blocks are not numbered 0..B-1")
@@ -138,6 +157,34 @@ def desc_from_keras_json(doc):
     eps = {cfg[n]["epsilon"] for n, v in r.items() if _is_bn(v)}
     if eps != {0.001}:
         raise NotSupported("BatchNormalization epsilon %s" % sorted(eps))
+    # squeeze-excite (model.py:101-126): Dense(S, relu, no bias) -> Dense(F, sigmoid, no bias)
+    se = {cfg[n]["units"] for n, v in r.items() if v.endswith("_se_compress")}
+    if len(se) > 1:
+        raise NotSupported("squeeze-excite units differ between blocks")
+    for n, v in r.items():
+        if _is_se(v):
+            want = "relu" if v.endswith("compress") else "sigmoid"
+            if cfg[n].get("use_bias") or cfg[n].get("activation") != want:
+                raise NotSupported("squeeze-excite layer %s is not Dense(%s, no bias)" % (n, want))
+    n_se = sum(1 for v in r.values() if v.endswith("_se_compress"))
+    if n_se not in (0, len(blocks)):
+        raise NotSupported("squeeze-excite on some blocks only")
+    # global-pooling value head (model.py:262-271): Concatenate([GAP(trunk), flatten(value conv)])
+    gap = False
+    for n in cfg:
+        if cls[n] == "GlobalAveragePooling2D" and not n.startswith("ResLayer_"):
+            gap = True
+        if cls[n] == "Concatenate":
+            srcs = _inbound(by_name[n])
+
+            def origin(x):
+                while cls[x] in ("Flatten", "Reshape", "Activation", "BatchNormalization", "Dropout"):
+                    x = _inbound(by_name[x])[0]
+                return cls[x]
+            if [origin(x) for x in srcs] != ["GlobalAveragePooling2D", "Conv2D"]:
+                raise NotSupported("concatenated value head %s (only the GAP-first pooling head)" % n)
+    if v2 and not gap and any(cls[n] == "Concatenate" for n in cfg):
+        raise NotSupported("concat_all_layers value head")
     flat = [c for n, c in cfg.items() if cls[n] == "Flatten"]
     dfs = {c.get("data_format") for c in flat}
     if len(dfs) != 1:
@@ -151,7 +198,9 @@ def desc_from_keras_json(doc):
     return NetDesc(input_channels=C, input_columns=H, input_rows=W, cnn_filter_size=F, residual_layers=len(blocks),
                    policy_dist_count=P, value_hidden_size=cfg[hidden]["units"], num_values=cfg[value]["units"],
                    cnn_kernel_size=k, leaky_relu=leaky, flatten_nchw=flatten_nchw, conv_bias=conv_bias.pop(),
-                   value_bn="value_bn" in r.values(), value_sigmoid=vact == "sigmoid")
+                   value_bn="value_bn" in r.values(), value_sigmoid=vact == "sigmoid",
+                   resnet_v2=v2, initial_bn="initial_bn" in r.values(), se_units=se.pop() if se else 0,
+                   global_pooling_value=gap, initial_kernel_size=0 if k0 == default_k0 else k0)
 
 
 def weights_from_keras(doc, layer_weights):
@@ -168,6 +217,8 @@ def weights_from_keras(doc, layer_weights):
             by_role[role] = ws[0]
             if desc.conv_bias:
                 by_role[role + "_bias"] = ws[1]
+        elif _is_se(role):
+            by_role[role] = ws[0]
         elif role.startswith("policy"):
             by_role[role] = ws[0]
             by_role[role.replace("_dense", "_bias")] = ws[1]
@@ -185,7 +236,7 @@ def weights_from_keras(doc, layer_weights):
 
 
 def keras_layer_shapes(doc):
-    """{layer name: [weight shapes]} a v1 model file's layers carry (for converters / tests)."""
+    """{layer name: [weight shapes]} a model file's layers carry (for converters / tests)."""
     desc = desc_from_keras_json(doc)
     spec = dict(weight_spec(desc))
     out = {}
@@ -194,6 +245,8 @@ def keras_layer_shapes(doc):
             out[name] = [spec[role + s] for s in ("_gamma", "_beta", "_mean", "_var")]
         elif _is_conv(role):
             out[name] = [spec[role]] + ([spec[role + "_bias"]] if desc.conv_bias else [])
+        elif _is_se(role):
+            out[name] = [spec[role]]
         elif role.startswith("policy"):
             out[name] = [spec[role], spec[role.replace("_dense", "_bias")]]
         elif role == "value_hidden":

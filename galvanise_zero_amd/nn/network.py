@@ -9,15 +9,24 @@ from .weights import to_blob
 
 
 def desc_from_conf(nn_model_conf, generation_descr=None):
-    """NNModelConfig (+ GenerationDescription.draw_head) -> NetDesc.  v1 topology only."""
+    """NNModelConfig (+ GenerationDescription.draw_head) -> NetDesc, as get_network_model builds it
+    (model.py:154-296): v1, or v2 with squeeze-excite (ratio 3, :190-197) and the global-pooling
+    value head (whose 1x1 conv has BN, :265-268)."""
     c = nn_model_conf
-    if c.resnet_v2 or c.squeeze_excite_layers or c.global_pooling_value or c.concat_all_layers:
-        raise NotImplementedError("only the v1 residual topology (resnet_v2=False) has a HIP forward")
+    if c.concat_all_layers:
+        raise NotImplementedError("concat_all_layers value head (model.py:251-260) has no HIP forward")
+    if c.squeeze_excite_layers and not c.resnet_v2:
+        raise ValueError("squeeze_excite_layers needs resnet_v2 (model.py:202)")
+    se = c.cnn_filter_size // 3 if (c.resnet_v2 and c.squeeze_excite_layers) else 0
+    if se:
+        assert se > 8, "model.py:111: filter_size // ratio > 8"
     draw = bool(generation_descr is not None and generation_descr.draw_head)
     return NetDesc(input_channels=c.input_channels, input_columns=c.input_columns, input_rows=c.input_rows,
                    cnn_filter_size=c.cnn_filter_size, residual_layers=c.residual_layers,
                    policy_dist_count=list(c.policy_dist_count), value_hidden_size=c.value_hidden_size,
-                   num_values=3 if draw else 2, cnn_kernel_size=c.cnn_kernel_size, leaky_relu=c.leaky_relu)
+                   num_values=3 if draw else 2, cnn_kernel_size=c.cnn_kernel_size, leaky_relu=c.leaky_relu,
+                   resnet_v2=bool(c.resnet_v2), se_units=se, global_pooling_value=bool(c.global_pooling_value),
+                   value_bn=bool(c.global_pooling_value))
 
 
 class HipModel(object):

@@ -15,8 +15,8 @@ from .desc import NetDesc, weight_spec
 def random_weights(desc: NetDesc, seed: int, bias_std: float = 0.0, res_gamma: float = 1.0):
     """Returns an ordered dict-like list [(name, float32 array)] following weight_spec().
 
-    ``res_gamma`` scales the gamma of each residual block's second BN (the branch added to the skip
-    path).  At 1.0 the residual stream of a deep random net grows with depth until every softmax
+    ``res_gamma`` scales the branch each residual block adds to the skip path: the gamma of the v1
+    block's second BN, the v2 block's second conv kernel.  At 1.0 the residual stream of a deep random net grows with depth until every softmax
     saturates (outputs 0/1), which hides numerical differences; parity tests of the 10-20 block
     configs use 0.15 so the outputs stay in the interior.
     """
@@ -26,6 +26,8 @@ def random_weights(desc: NetDesc, seed: int, bias_std: float = 0.0, res_gamma: f
         if len(shape) == 4:  # conv kernels, HWIO
             fan_in = shape[0] * shape[1] * shape[2]
             w = rng.normal(0.0, np.sqrt(2.0 / fan_in), size=shape)
+            if desc.resnet_v2 and name.endswith("_conv2"):
+                w = w * res_gamma
         elif name.endswith("_gamma"):
             w = rng.uniform(0.5, 1.5, size=shape)
             if name.endswith("_bn1_gamma"):

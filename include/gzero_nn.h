@@ -45,6 +45,13 @@ typedef struct gz_net_desc {
      *   product as hi*hi + hi*lo + lo*hi on the MFMA (~16 significant bits per operand, fp32
      *   accumulation); F <= 128.  The heads are fp32 in both modes. */
     int precision;
+    /* v2 (pre-activation) trunk, model.py:78-151 (the reference's features=True templates and its
+     * non-legacy model files); all zero = v1. */
+    int resnet_v2;                            /* blocks BN-act-conv-BN-act-conv [SE], add, no act    */
+    int initial_kernel;                       /* 1 or 3; 0 = model.py's (1 for v2, 3 for v1)        */
+    int initial_bn;                           /* v2: BN + act after the initial conv (0: bare conv)  */
+    int se_units;                             /* squeeze-excite compress units, 0 = none (<= 64)     */
+    int global_pooling_value;                 /* value features = [trunk channel means (F), conv (HW)] */
 } gz_net_desc;
 
 #define GZ_PRECISION_BF16 1

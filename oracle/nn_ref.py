@@ -17,6 +17,12 @@ executed by Keras 2.2 / TF 1.12 ``predict_on_batch`` (``src/ggpzero/util/cppinte
 * Legacy v1 model files (data/breakthrough/models/x6_102.json, keras 2.1.3): Conv2D(use_bias=True)
   everywhere (``conv_bias``), BatchNormalization after the value head's conv (``value_bn``), value
   Dense with sigmoid (``value_sigmoid``).
+* v2 (``resnet_v2``) model.py:78-151, 171-198: initial 1x1 ``conv2d_block`` (BN + act, or a bare conv
+  in older files: ``initial_bn=False``), blocks BN-act-conv-BN-act-conv, squeeze-excite
+  (``se_block`` :101-126: GlobalAveragePooling2D -> Dense(S, relu, no bias) -> Dense(F, sigmoid, no
+  bias) -> multiply), add without activation (:147); dropout is the identity at inference.
+* ``global_pooling_value`` model.py:262-271: value features = concat(GAP(trunk) [F], flatten(value
+  1x1 conv + BN + act) [HW]).
 
 Arithmetic is float64 (the fp32 TF result is within ~1e-6 of it); outputs are float32 like
 ``predict_on_batch``.  Parity of the reference NN itself is *unpinned*: no reference test holds a
@@ -88,12 +94,24 @@ def forward(desc, weights, planes):
         return y
 
     x = np.transpose(planes.astype(np.float64), (0, 2, 3, 1))     # NHWC
-    x = _act(_bn(conv(x, "initial_conv"), w, "initial_bn"), leaky)
+    v2 = getattr(desc, "resnet_v2", False)
+    x = conv(x, "initial_conv")
+    if not v2 or desc.initial_bn:
+        x = _act(_bn(x, w, "initial_bn"), leaky)
     for i in range(desc.residual_layers):
         t = x
-        y = _act(_bn(conv(x, "res%d_conv0" % i), w, "res%d_bn0" % i), leaky)
-        y = _bn(conv(y, "res%d_conv1" % i), w, "res%d_bn1" % i)
-        x = _act(t + y, leaky)
+        if v2:
+            y = conv(_act(_bn(x, w, "res%d_bn1" % i), leaky), "res%d_conv1" % i)
+            y = conv(_act(_bn(y, w, "res%d_bn2" % i), leaky), "res%d_conv2" % i)
+            if desc.se_units:
+                m = y.mean(axis=(1, 2))                                               # [N, F]
+                h = np.maximum(m @ w["res%d_se_compress" % i].astype(np.float64), 0.0)
+                y = y * _sigmoid(h @ w["res%d_se_gating" % i].astype(np.float64))[:, None, None, :]
+            x = t + y
+        else:
+            y = _act(_bn(conv(x, "res%d_conv0" % i), w, "res%d_bn0" % i), leaky)
+            y = _bn(conv(y, "res%d_conv1" % i), w, "res%d_bn1" % i)
+            x = _act(t + y, leaky)
     outs = []
     for r in range(desc.role_count):
         h = _act(_bn(conv(x, "policy%d_conv" % r), w, "policy%d_bn" % r), leaky)
@@ -104,8 +122,10 @@ def forward(desc, weights, planes):
     if getattr(desc, "value_bn", False):
         v = _bn(v, w, "value_bn")
     v = _act(v, leaky)
-    hid = _act(_flatten(v, desc.flatten_nchw) @ w["value_hidden"].astype(np.float64)
-               + w["value_hidden_bias"], leaky)
+    flat = _flatten(v, desc.flatten_nchw)
+    if getattr(desc, "global_pooling_value", False):
+        flat = np.concatenate([x.mean(axis=(1, 2)), flat], axis=1)
+    hid = _act(flat @ w["value_hidden"].astype(np.float64) + w["value_hidden_bias"], leaky)
     val = hid @ w["value_dense"].astype(np.float64) + w["value_bias"]
     outs.append(_value_out(desc, val))
     return outs
@@ -134,6 +154,7 @@ def _fold(w, conv, bn):
 
 
 def forward_bf16_emulated(desc, weights, planes):
+    assert not getattr(desc, "resnet_v2", False), "v1 only (v2 nets are checked against forward())"
     w = dict(weights)
     leaky = desc.leaky_relu
     x = bf16_round(np.transpose(planes, (0, 2, 3, 1))).astype(np.float64)

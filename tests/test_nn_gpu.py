@@ -51,8 +51,8 @@ VARIANTS = {
                              value_sigmoid=True),
 }
 # the reference's own model file breakthrough/models/x6_102.json as the importer reads it
-# (tests/golden/keras_v1_descs.json, nn/keras_model.py): 10 x 128 with the legacy flags
-with open(os.path.join(os.path.dirname(__file__), "golden", "keras_v1_descs.json")) as _f:
+# (tests/golden/keras_descs.json, nn/keras_model.py): 10 x 128 with the legacy flags
+with open(os.path.join(os.path.dirname(__file__), "golden", "keras_descs.json")) as _f:
     VARIANTS["x6_102_json"] = NetDesc(**json.load(_f)["breakthrough/models/x6_102.json"]["desc"])
 DEEP = {"cfg3", "cfg4", "cfg5", "x6_102_json"}       # residual gamma damped so the softmaxes do not saturate
 BIG = {"cfg4", "cfg5", "b2_13x13_f256", "b0_10x10_f256_v3"}   # oracle batch sizes kept small

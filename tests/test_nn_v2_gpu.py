@@ -1,0 +1,139 @@
+"""GPU parity of the v2 (pre-activation, squeeze-excite, global-pooling value head) forward
+(trunk_kernel_v2 via the C-ABI) against the float64 oracle (oracle/nn_ref.forward, whose v2 path is
+pinned against the reference's model-file layer graphs in tests/test_keras_model.py).
+
+Networks: every v2 model file of the reference the importer reads (tests/golden/keras_descs.json:
+bare or BN'd 1x1 / 3x3 initial convs, SE with 1 unit, GAP value heads with and without BN, sigmoid
+and softmax values, 6x6 .. 13x13 boards, F = 96 / 112 / 128 on the 128-filter kernels) and the
+reference's features=True templates (SE with F // 3 units, templates.py:62-65) on the BASELINE games,
+random-init weights (the reference's .h5 files are absent).
+
+Tolerances, stated against the float64 oracle, ~3x the worst measured on MI355X over these nets
+(profiles/r02j_v2_gpu_tests.log): bf16 mode max 0.0308 / mean 0.0062 (draughts f1_581, 10 blocks
+behind a 3x3 initial conv); fp32 mode (split operands, boards <= 64 positions) max 1.3e-6 / mean
+2.9e-7 / row KL 1.2e-7.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from galvanise_zero_amd.nn.desc import NetDesc
+from galvanise_zero_amd.nn.weights import random_planes, random_weights, to_blob
+from oracle import nn_ref
+
+pytestmark = pytest.mark.gpu
+
+TOL_V2_BF16 = (9.3e-2, 1.9e-2)   # max |err|, mean |err|
+TOL_FP32 = (4e-6, 1e-6)
+TOL_FP32_KL = 4e-7               # max over rows of KL(oracle || kernel)
+RES_GAMMA = 0.3                  # damps the v2 stream's growth so the softmaxes stay in the interior
+
+with open(os.path.join(os.path.dirname(__file__), "golden", "keras_descs.json")) as _f:
+    FILES = {k: NetDesc(**v["desc"]) for k, v in json.load(_f).items() if "desc" in v and v["desc"]["resnet_v2"]}
+
+
+def _err(a, b):
+    d = np.abs(a.astype(np.float64) - b.astype(np.float64))
+    return float(d.max()), float(d.mean())
+
+
+def _kl(ref, got):
+    r = np.clip(ref.astype(np.float64), 1e-30, None)
+    g = np.clip(got.astype(np.float64), 1e-30, None)
+    return float((r * np.log(r / g)).sum(axis=1).max())
+
+
+def _check(tag, desc, w, x, device, precision, tol, kl_tol=None):
+    from galvanise_zero_amd._native import HipNet
+    net = HipNet(desc, device, precision)
+    net.set_weights(to_blob(w))
+    got = net.forward(x)
+    ref = nn_ref.forward(desc, w, x)
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert g.shape == r.shape and np.all(np.isfinite(g))
+        er = _err(g, r)
+        sig = desc.value_sigmoid and i == len(got) - 1
+        kl = 0.0 if sig else _kl(r, g)
+        print("v2 %s %s n=%d out%d vs_ref max %.3g mean %.3g kl %.3g" % (tag, precision, x.shape[0], i, er[0], er[1], kl))
+        assert er[0] <= tol[0] and er[1] <= tol[1], (tag, precision, i, er)
+        if kl_tol is not None:
+            assert kl <= kl_tol, (tag, precision, i, kl)
+    net.close()
+
+
+@pytest.mark.parametrize("key", sorted(FILES))
+def test_v2_model_files(key, hip_device):
+    desc = FILES[key]
+    w = random_weights(desc, 7919, bias_std=0.2, res_gamma=RES_GAMMA)
+    for n in (1, 19):
+        x = random_planes(desc, n, 100 + n)
+        _check(key, desc, w, x, hip_device, "bf16", TOL_V2_BF16)
+        if desc.hw <= 64:
+            _check(key, desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
+
+
+GEOM_GAMES = ["breakthroughSmall", "breakthrough", "reversi", "hexLG13", "amazons_10x10"]
+
+
+def _template_desc(game, hint):
+    from galvanise_zero_amd.defs import templates
+    from galvanise_zero_amd.nn.bases import GdlBasesTransformer
+    from galvanise_zero_amd.nn.network import desc_from_conf
+    from galvanise_zero_amd.sm import get_sm
+    gen = templates.default_generation_desc(game, num_previous_states=1)
+    t = GdlBasesTransformer(get_sm(game), gen)
+    return desc_from_conf(templates.nn_model_config_template(game, hint, t, features=True), gen)
+
+
+@pytest.mark.parametrize("hint", ["small", "medium", "large"])
+@pytest.mark.parametrize("game", GEOM_GAMES)
+def test_v2_templates(game, hint, hip_device):
+    desc = _template_desc(game, hint)
+    assert desc.resnet_v2 and desc.se_units == desc.cnn_filter_size // 3 and desc.global_pooling_value
+    w = random_weights(desc, 7919, bias_std=0.2, res_gamma=RES_GAMMA)
+    x = random_planes(desc, 9, 31)
+    _check("%s/%s" % (game, hint), desc, w, x, hip_device, "bf16", TOL_V2_BF16)
+    if desc.hw <= 64:
+        _check("%s/%s" % (game, hint), desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
+
+
+V2_NETS = {"b1_58": FILES["breakthroughSmall/models/b1_58.json"], "f2_308": FILES["reversi_8x8/models/f2_308.json"],
+           "se21_8x8": NetDesc(5, 8, 8, 64, 3, [155, 155], resnet_v2=True, se_units=21, global_pooling_value=True,
+                               value_bn=True)}
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+@pytest.mark.parametrize("name", sorted(V2_NETS))
+def test_v2_batch_invariance(name, precision, hip_device):
+    """The squeeze-excite means are per board: rows do not depend on batch composition / slot, in
+    the one- and two-board-per-workgroup kernels alike (300 rows take the two-board kernel)."""
+    from galvanise_zero_amd._native import HipNet
+    desc = V2_NETS[name]
+    net = HipNet(desc, hip_device, precision)
+    net.set_weights(to_blob(random_weights(desc, 3, bias_std=0.2, res_gamma=RES_GAMMA)))
+    x = random_planes(desc, 300, 9)
+    full = net.forward(x)
+    perm = np.random.default_rng(0).permutation(300)[:37]
+    for a, b in zip(full, net.forward(x[perm])):
+        assert np.array_equal(a[perm], b)
+    for a, b in zip(full, net.forward(x[5:6])):
+        assert np.array_equal(a[5:6], b)
+
+
+@pytest.mark.parametrize("precision,variant", [("bf16", "11"), ("bf16", "21"), ("bf16", "12"), ("fp32", "11"),
+                                               ("fp32", "21")])
+def test_v2_kernel_variants_identical(precision, variant, hip_device, monkeypatch):
+    from galvanise_zero_amd._native import HipNet
+    desc = V2_NETS["f2_308"]
+    x = random_planes(desc, 33, 4)
+    w = to_blob(random_weights(desc, 5, bias_std=0.2, res_gamma=RES_GAMMA))
+    net = HipNet(desc, hip_device, precision)
+    net.set_weights(w)
+    base = net.forward(x)
+    monkeypatch.setenv("GZ_KERNEL_VARIANT", variant)
+    vnet = HipNet(desc, hip_device, precision)
+    vnet.set_weights(w)
+    for a, b in zip(base, vnet.forward(x)):
+        assert np.array_equal(a, b)

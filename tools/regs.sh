@@ -1,6 +1,6 @@
 #!/bin/bash
 # Register / spill / LDS usage of every kernel of libgz_nn (device-only compile, no GPU needed).
-for tu in gz_nn trunk_f64 trunk_f128 trunk_f256; do
+for tu in gz_nn trunk_f64 trunk_f128 trunk_f256 trunk_f64_v2 trunk_f128_v2; do
 cd /tmp && /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -Wno-unused-parameter -I/root/repo/include \
   --cuda-device-only -c /root/repo/galvanise_zero_amd/csrc/nn/$tu.hip -o /tmp/gz_dev_$tu.o \
   -Rpass-analysis=kernel-resource-usage 2>&1 | python3 -c '
