@@ -137,3 +137,25 @@ def test_v2_kernel_variants_identical(precision, variant, hip_device, monkeypatc
     vnet.set_weights(w)
     for a, b in zip(base, vnet.forward(x)):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("game,key", [("breakthroughSmall", "breakthroughSmall/models/b1_58.json"),
+                                      ("reversi", "reversi_8x8/models/f2_308.json")])
+def test_v2_keras_dropin(game, key, hip_device):
+    """Manager.network_from_keras (the load_network replacement, manager.py:129-139) on a v2 model
+    file's layer graph and per-layer weights: predict_on_batch on the HIP forward equals the model
+    file's own graph evaluated layer by layer (tests/test_keras_model.keras_graph_forward)."""
+    from test_keras_model import _random_layer_weights, keras_graph_forward
+    from galvanise_zero_amd.nn.manager import Manager
+    with open(os.path.join(os.path.dirname(__file__), "golden", "keras_descs.json")) as f:
+        g = json.load(f)[key]
+    lw = _random_layer_weights(g["layers"], 11)
+    nn = Manager(device=hip_device).network_from_keras(game, g["graph"], lw)
+    desc = FILES[key]
+    x = random_planes(desc, 16, 5)
+    got = nn.get_model().predict_on_batch(x)
+    exp = keras_graph_forward(g["graph"], lw, x)
+    for i, (a, b) in enumerate(zip(got, exp)):
+        er = _err(a, b)
+        print("v2 keras drop-in %s out%d max %.3g mean %.3g" % (key, i, er[0], er[1]))
+        assert er[0] <= TOL_V2_BF16[0] and er[1] <= TOL_V2_BF16[1]
