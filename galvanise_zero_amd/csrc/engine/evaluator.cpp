@@ -765,10 +765,14 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
                 ok = false;
             }
             if (ok) {
+                // one draw per reaching child; only d's (at `rank`) is read
                 bool latched = false;
-                for (int j = 0; j < reach; ++j) {
-                    const double v = rng.get();
-                    if (j == rank && latch_d >= 0 && v > 0.1) latched = true;
+                if (latch_d >= 0) {
+                    rng.discard((uint64_t)rank);
+                    latched = rng.get() > 0.1;
+                    rng.discard((uint64_t)(reach - rank - 1));
+                } else {
+                    rng.discard((uint64_t)reach);
                 }
                 if (latched) {
                     ok = sep_no_d;
@@ -1285,7 +1289,7 @@ bool PuctEvaluator::spinPlayout() {
             std::abort();
         }
     } else if (latch) {
-        for (int j = 0; j < spin.reach; ++j) (void)rng.get();   // the root latch's per-child draws
+        rng.discard((uint64_t)spin.reach);   // the root latch's per-child draws (values unused)
     }
 
     // treePlayout (evaluator.cpp:658-720): root -> chosen (finalised terminal) -> backup
