@@ -101,8 +101,13 @@ __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
 
 // The board geometry at run time (kernels are compiled per filter count and position-tile count):
 // p / W as (p * ceil(65536 / W)) >> 16, exact for W <= 32 and p < 1024 (checked on the host).
+constexpr int kMaxPTN = 11;        // position tiles of the largest compiled board (13 x 13)
 struct Board {
     int H, W, npos, wmagic;
+    // per lane and position tile pt (position p = 16 pt + lane % 16): bit tap (0-8) says whether p
+    // is on the board and its neighbour at that 3x3 tap exists (set once per kernel), so a conv's
+    // per-tap B-fragment addresses need no division, multiply or divergent bounds check
+    int tapmask[kMaxPTN];
     __device__ __forceinline__ int row(int p) const { return (p * wmagic) >> 16; }
 };
 
@@ -306,10 +311,9 @@ __device__ __forceinline__ TapAddr tap_base(int tap, int pt, int lane, const Boa
     const int li = lane & 15, g = lane >> 4;
     const int dy = tap / 3 - 1, dx = tap % 3 - 1;
     const int p = 16 * pt + li;
-    const int r = bd.row(p);
-    const int y = r + dy, x = p - r * bd.W + dx;
-    const bool ok = p < bd.npos && (unsigned)y < (unsigned)bd.H && (unsigned)x < (unsigned)bd.W;
-    const int qv = p + dy * bd.W + dx;
+    static_assert(PTN <= kMaxPTN, "board larger than the tap masks");
+    const int qv = p + (dy * bd.W + dx);                 // the (virtual) neighbour position
+    const bool ok = (bd.tapmask[pt] >> tap) & 1;
     const int rot = G::WRAP ? (((g + swz(qv)) & 15) << 4) : ((g + swz(qv)) << 4);
     return TapAddr{(ok ? qv : bd.npos) * G::ROWS, rot};
 }
@@ -378,6 +382,9 @@ __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, P
                 __builtin_amdgcn_sched_group_barrier(0x008, CT * (P2 == 2 ? 3 : 1), 0);   // MFMA
                 __builtin_amdgcn_sched_group_barrier(0x100, P2, 0);                       // DS read
             }
+            // k-step boundary: nothing crosses it, so the next k-step's B reads stay one k-step
+            // ahead of their MFMAs (double buffer) and scheduling regions stay one k-step long
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
@@ -516,7 +523,22 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     constexpr int P2 = G::P2;
     constexpr int PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, kThreads = 256;
     const int NPOS = kp.npos, H = kp.H, W = kp.W;     // the board (NPOS <= G::NPOS)
-    const Board bd{H, W, NPOS, kp.wmagic};
+    Board bd{H, W, NPOS, kp.wmagic, {}};
+    {
+        const int li = threadIdx.x & 15;
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) {
+            const int p = 16 * pt + li;
+            const int r = bd.row(p), x = p - r * W;
+            int m = 0;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int y = r + tap / 3 - 1, xx = x + tap % 3 - 1;
+                if (p < NPOS && (unsigned)y < (unsigned)H && (unsigned)xx < (unsigned)W) m |= 1 << tap;
+            }
+            bd.tapmask[pt] = m;
+        }
+    }
     constexpr int ACT = G::ACT_BYTES;
 
     constexpr bool SI = G::SI, RG = G::RG;
