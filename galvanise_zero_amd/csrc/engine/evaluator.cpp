@@ -1005,7 +1005,7 @@ int PuctEvaluator::treePlayout(PuctNode* current, Path& path) {
 // "converged" (the two most visited children are wins with equal scores) and runs until enough NN
 // evaluations accumulate -- up to millions of playouts per move, nearly all of them root -> win ->
 // backup with no evaluation (playoutMain, evaluator.cpp:744-886).  Such a playout only needs the
-// scores of the few children that can still win the selection: spinPlayout runs one playout of
+// scores of the few children that can still win the selection: spinRun runs playouts of
 // that form with the reference's arithmetic and RNG consumption (the root-latch draw per reaching
 // child), and returns false whenever the proof below does not hold or another child wins the
 // selection, after which the ordinary treePlayout runs.
@@ -1195,118 +1195,174 @@ bool PuctEvaluator::spinBuild() {
     return false;
 }
 
-bool PuctEvaluator::spinPlayout() {
-    if (!spin_fast_enabled()) return false;
+// Up to `limit` consecutive spin playouts (1 unless `multi`: playoutMain passes multi when none of
+// its loop conditions can change over a run of spin playouts, see there); a run continues past the
+// first playout only inside an epoch whose converged() is proved false.  Returns how many playouts
+// ran (0: the next playout takes the ordinary path).  Each playout is spinPlayout's selection and
+// backup() specialised to the path root -> finalised win: the same float / double operations in the
+// same order, with no path vector and no per-playout loop-top bookkeeping.
+int PuctEvaluator::spinRun(int limit, bool multi) {
+    if (!spin_fast_enabled() || limit <= 0) return 0;
+    if (spin.fail_next) {   // the playout after a run failed the fast path: ordinary path now
+        spin.fail_next = false;
+        spin.valid = false;
+        return 0;
+    }
     PuctNode* node = root;
     if (!spin.valid || spin.root != node || node->visits >= spin.v_end) {
-        if (spin.root == node && node->visits < spin.retry_at) return false;
+        if (spin.root == node && node->visits < spin.retry_at) return 0;
         if (!spinBuild()) {
             spin.root = node;
             spin.retry_at = node->visits + 8;
-            return false;
+            return 0;
         }
     }
+    if (!multi || !spin.conv_false) limit = 1;
     const int lead = node->lead_role_index;
-    if (node->inflight_visits != 0 ||
-        (!node->dirichlet_noise_set && conf->dirichlet_noise_pct >= 0 && node->getCurrentScore(lead) <= 0.95)) {
-        spin.valid = false;
-        return false;
-    }
-
-    // selectChild (evaluator.cpp:341-517) restricted to the wins and the watched candidates
-    setPuctConstant(node, 0);
-    const double sqrt_node_visits = std::sqrt(node->visits + 1);
+    const int role_count = sm->roleCount();
     PuctNodeChild* cs = node->children();
-    const bool latch = node->visits > 1000 && node->visits < 40000000;
     const float limit_latch_root = 0.66;
-    float prior_score = 0.f;
-    if (spin.watch_prior) {
-        // priorScore (evaluator.cpp:1195-1224): the top-visits child is a win; the policy sum of
-        // the visited children accumulates in child order
-        float total_policy_visited = 0.0;
-        for (int k = 0; k < spin.nvisited; ++k) total_policy_visited += cs[spin.visited[k]].policy_prob;
-        prior_score = spin.win_score;
-        float fpu_reduction = conf->fpu_prior_discount_root;
-        if (fpu_reduction > 0) {
-            fpu_reduction *= std::sqrt(total_policy_visited);
-            prior_score -= fpu_reduction;
+    const bool verify = verify_fastpath();
+    int done = 0;
+    while (done < limit && node->visits < spin.v_end) {
+        // a playout that cannot take the fast path ends the run; it is the ordinary path's, at once
+        // when it is the run's first, else at the next call (after playoutMain's loop-top checks)
+        auto fail = [&]() {
+            if (done == 0) spin.valid = false;
+            else spin.fail_next = true;
+        };
+        if (node->inflight_visits != 0 ||
+            (!node->dirichlet_noise_set && conf->dirichlet_noise_pct >= 0 && node->getCurrentScore(lead) <= 0.95)) {
+            fail();
+            break;
         }
-    }
-    float best_score = -1;
-    int best = -1;
-    bool best_win = false;
-    double best_exact = 0.0;
-    for (int k = 0; k < spin.ncand; ++k) {
-        const int i = spin.cand[k];
-        const uint8_t kind = spin.cand_kind[k];
-        PuctNodeChild* c = cs + i;
-        const PuctNode* cn = c->to_node;
-        if (kind == SpinEpoch::kWin && latch && c->traversals > 16 &&
-            c->traversals > node->visits * limit_latch_root) {
-            spin.valid = false;
-            return false;
-        }
-        const int traversals = c->traversals + 1;
-        const double inflight_visits = cn != nullptr ? cn->inflight_visits : 0;
-        double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
-                                   (traversals + inflight_visits);
-        double child_score = prior_score;
-        if (cn != nullptr) {
-            child_score = cn->getCurrentScore(lead);
-            if (kind == SpinEpoch::kWin) child_score *= 1.0f + node->puct_constant;
-            else if (cn->is_finalised) exploration_score = 0.0;
-        }
-        const double score = child_score + exploration_score;
-        if (score > best_score) {   // the reference loop (evaluator.cpp:487-490), float best_score
-            best = i;
-            best_score = score;
-            best_win = kind == SpinEpoch::kWin;
-            best_exact = score;
-        }
-    }
-    // a watched candidate wins (its playout descends: ordinary path), or the result is not
-    // separated from the unwatched bound
-    if (!best_win || !(spin.unwatched_bound < best_exact) || !(spin.unwatched_bound <= (double)(float)best_exact)) {
-        spin.valid = false;
-        return false;
-    }
-    PuctNodeChild* chosen = cs + best;
 
-    if (verify_fastpath()) {
-        // the ordinary selection from the same RNG state must pick the same child
-        const Rng before = rng;
-        for (int j = 0; latch && j < spin.reach; ++j) (void)rng.get();
-        const Rng after = rng;
-        rng = before;
-        Path tmp;
-        PuctNodeChild* ref = selectChild(node, tmp);
-        if (ref != chosen || !(rng == after)) {
-            std::fprintf(stderr, "gz spin fast-path mismatch (visits %u)\n", node->visits);
-            std::abort();
+        // selectChild (evaluator.cpp:341-517) restricted to the wins and the watched candidates
+        setPuctConstant(node, 0);
+        const double sqrt_node_visits = std::sqrt(node->visits + 1);
+        const bool latch = node->visits > 1000 && node->visits < 40000000;
+        float prior_score = 0.f;
+        if (spin.watch_prior) {
+            // priorScore (evaluator.cpp:1195-1224): the top-visits child is a win; the policy sum of
+            // the visited children accumulates in child order
+            float total_policy_visited = 0.0;
+            for (int k = 0; k < spin.nvisited; ++k) total_policy_visited += cs[spin.visited[k]].policy_prob;
+            prior_score = spin.win_score;
+            float fpu_reduction = conf->fpu_prior_discount_root;
+            if (fpu_reduction > 0) {
+                fpu_reduction *= std::sqrt(total_policy_visited);
+                prior_score -= fpu_reduction;
+            }
         }
-        if (spin.conv_false && converged(conf->converged_visits)) {
-            std::fprintf(stderr, "gz spin fast-path: converged() is true\n");
-            std::abort();
+        float best_score = -1;
+        int best = -1;
+        bool best_win = false, latched_win = false;
+        double best_exact = 0.0;
+        for (int k = 0; k < spin.ncand; ++k) {
+            const int i = spin.cand[k];
+            const uint8_t kind = spin.cand_kind[k];
+            PuctNodeChild* c = cs + i;
+            const PuctNode* cn = c->to_node;
+            if (kind == SpinEpoch::kWin && latch && c->traversals > 16 &&
+                c->traversals > node->visits * limit_latch_root) {
+                latched_win = true;
+                break;
+            }
+            const int traversals = c->traversals + 1;
+            const double inflight_visits = cn != nullptr ? cn->inflight_visits : 0;
+            double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
+                                       (traversals + inflight_visits);
+            double child_score = prior_score;
+            if (cn != nullptr) {
+                child_score = cn->getCurrentScore(lead);
+                if (kind == SpinEpoch::kWin) child_score *= 1.0f + node->puct_constant;
+                else if (cn->is_finalised) exploration_score = 0.0;
+            }
+            const double score = child_score + exploration_score;
+            if (score > best_score) {   // the reference loop (evaluator.cpp:487-490), float best_score
+                best = i;
+                best_score = score;
+                best_win = kind == SpinEpoch::kWin;
+                best_exact = score;
+            }
         }
-    } else if (latch) {
-        rng.discard((uint64_t)spin.reach);   // the root latch's per-child draws (values unused)
-    }
+        // a win reaches the root latch, a watched candidate wins (its playout descends: ordinary
+        // path), or the result is not separated from the unwatched bound
+        if (latched_win || !best_win || !(spin.unwatched_bound < best_exact) ||
+            !(spin.unwatched_bound <= (double)(float)best_exact)) {
+            fail();
+            break;
+        }
+        PuctNodeChild* chosen = cs + best;
 
-    // treePlayout (evaluator.cpp:658-720): root -> chosen (finalised terminal) -> backup
-    PuctNode* leaf = chosen->to_node;
-    Path& path = spin_path;
-    path.clear();
-    path.emplace_back(node, chosen, chosen);
-    node->inflight_visits++;
-    node->syncParent();
-    path.emplace_back(leaf, nullptr, nullptr);
-    stats.playouts_finals++;
-    float scores[kMaxRoles];
-    for (int ii = 0; ii < sm->roleCount(); ii++) scores[ii] = leaf->getCurrentScore(ii);
-    backup(scores, path);
-    stats.num_tree_playouts++;
-    total_tree_playouts++;
-    return true;
+        if (verify) {
+            // the ordinary selection from the same RNG state must pick the same child
+            const Rng before = rng;
+            for (int j = 0; latch && j < spin.reach; ++j) (void)rng.get();
+            const Rng after = rng;
+            rng = before;
+            Path tmp;
+            PuctNodeChild* ref = selectChild(node, tmp);
+            if (ref != chosen || !(rng == after)) {
+                std::fprintf(stderr, "gz spin fast-path mismatch (visits %u)\n", node->visits);
+                std::abort();
+            }
+            if (spin.conv_false && converged(conf->converged_visits)) {
+                std::fprintf(stderr, "gz spin fast-path: converged() is true\n");
+                std::abort();
+            }
+        } else if (latch) {
+            rng.discard((uint64_t)spin.reach);   // the root latch's per-child draws (values unused)
+        }
+
+        // treePlayout (evaluator.cpp:658-720): root -> chosen (finalised terminal), then backup()
+        // over that two-element path (backup_finalised is off in an epoch)
+        PuctNode* leaf = chosen->to_node;
+        node->inflight_visits++;
+        node->syncParent();
+        stats.playouts_finals++;
+        float scores[kMaxRoles];
+        for (int ii = 0; ii < role_count; ii++) scores[ii] = leaf->getCurrentScore(ii);
+        // the leaf (finalised): its scores propagate unchanged
+        leaf->visits++;
+        if (leaf->inflight_visits > 0) leaf->inflight_visits--;
+        leaf->syncParent();
+        if (leaf->visits % 100 == 0) leaf->normaliseX();
+        // the root (never finalised inside an epoch)
+        for (int ii = 0; ii < role_count; ii++) {
+            float visits = node->visits;
+            if (visits > 100000) visits = 100000 + 0.1f * (visits - 100000);
+            const float score = ((visits * node->getCurrentScore(ii) + scores[ii]) / (visits + 1.0f));
+            node->setCurrentScore(ii, score);
+        }
+        node->visits++;
+        if (node->inflight_visits > 0) node->inflight_visits--;
+        node->syncParent();
+        chosen->traversals++;
+        if (node->visits > 23) {
+            const float cur_score = node->getCurrentScore(node->lead_role_index);
+            float apply, minimum;
+            if (cur_score > 0.3 && cur_score < 0.7) {
+                apply = 0.995;
+                minimum = 0.02f;
+            } else if (cur_score > 0.15 && cur_score < 0.85) {
+                apply = 0.9975;
+                minimum = 0.03f;
+            } else {
+                apply = 0.9975;
+                minimum = 0.10f;
+            }
+            if (chosen->policy_prob > minimum) {
+                chosen->policy_prob *= apply;
+                chosen->policy_prob = std::max(minimum, chosen->policy_prob);
+            }
+        }
+        if (node->visits % 100 == 0) node->normaliseX();
+        stats.num_tree_playouts++;
+        total_tree_playouts++;
+        ++done;
+    }
+    return done;
 }
 
 // evaluator.cpp:722-742
@@ -1332,6 +1388,7 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
 
     Path path;
     int evals_seen = stats.num_evaluations, quiet_playouts = 0;   // spin_yield_playouts (config.h)
+    spin.fail_next = false;   // a failure seen past the end of the last call is re-evaluated
     while (true) {
         const int our_role_index = root->lead_role_index;
         // converged() is pure (no RNG, no writes); the reference evaluates it every iteration, but
@@ -1361,20 +1418,30 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
             }
         }
 
+        // A run of spin playouts stands for that many iterations of this loop when none of the
+        // checks above can change within it: no think time or end time, the non-converged
+        // evaluation limit not reached (evaluations and node counts do not change in a spin
+        // playout), converged() proved false (spinRun), and the run ends at the next spin yield.
+        const bool multi = !use_think_time && end_time <= 0 && !root->is_finalised &&
+                           !(stats.num_evaluations > max_non_converged_evaluations) && number_of_nodes <= 50000000;
+        int limit = 1 << 20;
+        if (conf->spin_yield_playouts > 0) limit = conf->spin_yield_playouts - quiet_playouts;
         int depth = 2;
-        if (!spinPlayout()) {
+        int ran = spinRun(limit, multi);
+        if (ran == 0) {
             spin.valid = false;
             path.clear();
             depth = treePlayout(root, path);
+            ran = 1;
         }
         stats.playouts_max_depth = std::max(depth, stats.playouts_max_depth);
-        stats.playouts_total_depth += depth;
+        stats.playouts_total_depth += depth * ran;
 
         if (conf->spin_yield_playouts > 0) {
-            if (stats.num_evaluations != evals_seen) {
+            if (stats.num_evaluations != evals_seen) {   // (never after a spin run)
                 evals_seen = stats.num_evaluations;
                 quiet_playouts = 0;
-            } else if (++quiet_playouts >= conf->spin_yield_playouts) {
+            } else if ((quiet_playouts += ran) >= conf->spin_yield_playouts) {
                 quiet_playouts = 0;
                 scheduler->yield();
             }

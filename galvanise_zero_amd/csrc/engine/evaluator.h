@@ -118,9 +118,10 @@ private:
         double unwatched_bound = 0;  // upper bound of every unwatched candidate's score until v_end
         bool conv_false = false;     // converged() proved false for the epoch
         bool valid = false;
+        bool fail_next = false;      // spinRun: the next playout fails the fast path (seen in the last run)
     };
     bool spinBuild();
-    bool spinPlayout();
+    int spinRun(int limit, bool multi);
     SpinEpoch spin;
     Path spin_path;
 
