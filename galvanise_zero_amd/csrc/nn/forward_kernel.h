@@ -559,6 +559,28 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     const int co_base = wave * (F / 4);
     const int C = kp.C, K0 = kp.K0;
 
+    // The NB boards' input planes, fetched before anything else with 16-byte loads so that one round
+    // trip (pinned host memory over PCIe in the runner, HBM otherwise) covers every board: up to
+    // kPF float4 per thread per board, when the plane block is a whole number of aligned float4s
+    // (otherwise the staging loop below reads it)
+    constexpr int kPF = 4;
+    const int nf4 = (C * NPOS) >> 2;
+    const float* in_b[NB];
+    bool vec_b[NB];
+    float4 pf[NB][kPF];
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+        const bool live = board0 + bb < kp.n;
+        const int sg = find_segment(kp, board0 + bb);
+        in_b[bb] = live ? kp.seg[sg].planes + (size_t)(board0 + bb - kp.seg[sg].row0) * C * NPOS : nullptr;
+        vec_b[bb] = ((C * NPOS) & 3) == 0 && nf4 <= kPF * kThreads && ((uintptr_t)in_b[bb] & 15) == 0;
+#pragma unroll
+        for (int k = 0; k < kPF; ++k) {
+            const int i4 = tid + k * kThreads;
+            pf[bb][k] = (live && vec_b[bb] && i4 < nf4) ? ((const float4*)in_b[bb])[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+
     // prime the weight ring: stages 0 .. R-2 of the trunk stream
     const uint32_t woff = (uint32_t)((co_base + li) * G::ROWB + 16 * g);   // lane's fragment bytes within a k-step
     const int gmax = 2 * kp.B * G::NST - 1;
@@ -584,10 +606,14 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     const int imswz = ((K0 >> 3) < 16 ? (K0 >> 3) : 16) - 1;
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
-        const bool live = board0 + bb < kp.n;
-        const int sg = find_segment(kp, board0 + bb);
-        const float* in = kp.seg[sg].planes + (size_t)(board0 + bb - kp.seg[sg].row0) * C * NPOS;
-        for (int i = tid; i < C * NPOS; i += kThreads) sin[i] = live ? in[i] : 0.f;
+        const float* in = in_b[bb];
+        if (vec_b[bb]) {   // dead boards: zeros
+#pragma unroll
+            for (int k = 0; k < kPF; ++k)
+                if (tid + k * kThreads < nf4) ((float4*)sin)[tid + k * kThreads] = pf[bb][k];
+        } else {
+            for (int i = tid; i < C * NPOS; i += kThreads) sin[i] = in != nullptr ? in[i] : 0.f;
+        }
         __syncthreads();
         // IM[p][k], k = tap*C + c (a 1x1 initial conv: k = c), zero padded to K0: zero the image,
         // then one thread per (position, tap) copies its C channels (compile-time divisors only)

@@ -2,7 +2,7 @@
 # r02l: trunk kernel with per-lane tap masks and k-step scheduling barriers: NN GPU parity tests,
 # forward timings by launch size (bf16 / fp32), fixed vs per-block cost
 set -o pipefail
-T=gpurun_out/r02l
+T=gpurun_out/${1:-r02l}
 mkdir -p $T
 timeout -k 10 600 python -u -m pytest tests/test_nn_gpu.py tests/test_nn_v2_gpu.py -v -s --timeout 300 --timeout-method thread > $T/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error" $T/tests.log | head -20; exit 1; }
 tail -1 $T/tests.log
