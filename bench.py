@@ -256,6 +256,7 @@ def main():
     if args.precision is None:
         args.precision = "fp32" if desc.cnn_filter_size <= 128 else "bf16"
     net = HipNet(desc, device, args.precision)
+    heads_fused = net.heads_fused()
 
     # weights: rank 0 creates, RCCL broadcast of the blob (the only collective on the path)
     blob = torch.empty(net.weight_count, dtype=torch.float32, device="cuda")
@@ -355,12 +356,15 @@ def main():
                                                                    s1["rows"] - s1["large_rows"],
                                                                    s1["trunk_ms"] - s1["large_trunk_ms"]),
         }
+        # two-image trunk kernels run the dense heads themselves (no heads launch): their algorithmic
+        # work per leaf is then the whole forward's
+        kernel_flops = desc.flops_per_eval() if heads_fused else desc.flops_trunk()
         per_variant = {}
         for name, (vl, vr, vt) in variants.items():
             if vl > 0 and vt > 0:
                 wl, wr, wt = whole[name]
                 per_variant[name] = {"launches": vl, "rows_per_launch": vr / vl, "avg_kernel_ms": vt / vl,
-                                     "achieved_tflops": desc.flops_trunk() * vr / (vt / 1e3) / 1e12,
+                                     "achieved_tflops": kernel_flops * vr / (vt / 1e3) / 1e12,
                                      "whole_run": {"launches": wl, "rows_per_launch": wr / max(wl, 1),
                                                    "avg_kernel_ms": wt / max(wl, 1)}}
         dom = max(per_variant, key=lambda k: variants[k][2]) if per_variant else None
@@ -422,7 +426,7 @@ def main():
                          "traffic_source": TRAFFIC_SOURCE if args.config == 2 and dom in TRAFFIC_PER_LAUNCH else None,
                          "kernel": dom, "avg_kernel_ms": per_variant[dom]["avg_kernel_ms"] if dom else None,
                          "rows_per_launch": per_variant[dom]["rows_per_launch"] if dom else None,
-                         "flop_per_leaf_kernel": desc.flops_trunk(), "variants": per_variant,
+                         "flop_per_leaf_kernel": kernel_flops, "heads_fused": heads_fused, "variants": per_variant,
                          "launch_rows_mean": rows_per_launch,
                          "pools_per_launch": segments / launches if launches else None,
                          "forward_avg_ms": avg_fwd_s * 1e3,

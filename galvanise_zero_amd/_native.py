@@ -100,6 +100,8 @@ def nn_lib():
         lib.gz_net_stamp_avg.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
         lib.gz_net_flops_per_eval.restype = ctypes.c_double
         lib.gz_net_flops_per_eval.argtypes = [ctypes.c_void_p]
+        lib.gz_net_heads_fused.restype = ctypes.c_int
+        lib.gz_net_heads_fused.argtypes = [ctypes.c_void_p]
         lib.gz_nn_last_error.restype = ctypes.c_char_p
         lib._gz_typed = True
     return lib
@@ -209,6 +211,10 @@ class HipNet(object):
 
     def flops_per_eval(self):
         return self.lib.gz_net_flops_per_eval(self.handle)
+
+    def heads_fused(self):
+        """True when the large trunk variant runs the dense heads itself (no heads_kernel launch)."""
+        return bool(self.lib.gz_net_heads_fused(self.handle))
 
     def close(self):
         if self.handle:

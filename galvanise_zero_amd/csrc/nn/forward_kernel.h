@@ -871,12 +871,21 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     // features in the model's Flatten order go to the scratch for heads_kernel ----------------
     const int HC = 2 * kp.R + 1;
     float* hpart = (float*)SCR;                                  // [4][HC][NPOS]
+    // FUSE (two-image kernels): the features stay in LDS, fk = [FS][NB], and the dense heads run
+    // here; single-image kernels write them to the device scratch for heads_kernel
+    constexpr bool FUSE = !SI;
+    float* fk = (float*)(SCR + align16(4 * HC * NPOS * 4));
+    float* lg = fk + align16(kp.FS * NB * 4) / 4;
+    // feature k of board bb
+    auto feat_at = [&](int bb, int k) -> float& {
+        if constexpr (FUSE) return fk[k * NB + bb];
+        else return kp.feat[(size_t)(board0 + bb) * kp.FS + k];
+    };
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
         const int board = board0 + bb;
         if (kp.gapF && board < kp.n) {   // pooling value head: the trunk's channel means (model.py:263)
             const float inv = 1.f / (float)NPOS;
-            float* fo = kp.feat + (size_t)board * kp.FS + 2 * kp.R * NPOS;
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
                 const f32x4 sm = board_channel_sum<F, PTN, NB, P>(acc, ct, bb, li, NPOS);
@@ -884,7 +893,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                 if (li == 0)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        if (co + r < kp.gapF) fo[co + r] = sm[r] * inv;
+                        if (co + r < kp.gapF) feat_at(bb, 2 * kp.R * NPOS + co + r) = sm[r] * inv;
             }
         }
         for (int h = 0; h < HC; ++h) {
@@ -909,7 +918,6 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         }
         __syncthreads();
         if (board < kp.n) {
-            float* fo = kp.feat + (size_t)board * kp.FS;
             for (int i = tid; i < HC * NPOS; i += kThreads) {
                 const int h = i / NPOS, p = i - (i / NPOS) * NPOS;
                 float s = kp.bh[h];
@@ -919,13 +927,17 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                 if (h < 2 * kp.R) {
                     const int r = h >> 1, c = h & 1;
                     const int idx = kp.flatten_nchw ? c * NPOS + p : p * 2 + c;
-                    fo[r * 2 * NPOS + idx] = s;
+                    feat_at(bb, r * 2 * NPOS + idx) = s;
                 } else {
-                    fo[2 * kp.R * NPOS + kp.gapF + p] = s;
+                    feat_at(bb, 2 * kp.R * NPOS + kp.gapF + p) = s;
                 }
             }
         }
         __syncthreads();    // hpart is reused by the next board
+    }
+    if constexpr (FUSE) {
+        const int nb = kp.n - board0 < NB ? kp.n - board0 : NB;
+        dense_heads<NB>(kp, fk, lg, board0, nb);
     }
     GZ_STAMP(3);
 #undef GZ_STAMP
@@ -946,48 +958,39 @@ trunk_kernel_v2(const KParams kp) {
 }
 
 // ---- heads -------------------------------------------------------------------------------------
-// kHeadBoards boards per workgroup of 4 waves.  Dense layers in fp32: thread j owns output j (of
-// P_r or VH) for every board of the workgroup; the k-major weights are read coalesced, each once
-// per workgroup, and the features come from LDS as one broadcast float4 per k (k-major, board-minor
-// image).  Each board's sums run in a fixed k order: outputs are independent of batch composition.
-#ifdef GZNN_DEFINE_HEADS_KERNEL   // defined in one translation unit (gz_nn.hip)
-__global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
-    constexpr int BPW = kHeadBoards;
-    static_assert(BPW == 4, "one float4 of features per k, one softmax wave per board");
-    extern __shared__ __attribute__((aligned(16))) float hs[];
-    const int NPOS = kp.npos, FS = kp.FS;
+// Dense heads of BPW boards whose head features are in LDS, fk = [FS][BPW] (k-major, board-minor):
+// policy Dense + softmax per role, value MLP + softmax (sigmoid for legacy files); results straight
+// to the segments' buffers.  lg = LDS [BPW][LMAX].  Dense layers in fp32: thread j owns output j
+// (of P_r or VH) for every board; the k-major weights are read coalesced, once per call, and the
+// features come from LDS as one broadcast read per k.  Each board's sums run in a fixed k order with
+// the same operations for every BPW, so outputs do not depend on how boards are grouped (fused into
+// the trunk kernel with BPW = its NB, or in heads_kernel with BPW = 4).  Every thread of the
+// workgroup (4 waves) must call it; boards board0 .. board0 + nb - 1 are written.
+template <int BPW>
+__device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, float* lg, int board0, int nb) {
+    static_assert(BPW >= 1 && BPW <= 4, "one softmax wave per board");
+    const int NPOS = kp.npos;
     const int LMAX = kp.maxP > kp.VH ? kp.maxP : kp.VH;
-    float* fk = hs;                       // [FS][BPW]
-    float* lg = hs + FS * BPW;            // [BPW][LMAX]
-    float* red = lg + BPW * LMAX;         // [BPW][4]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int board0 = blockIdx.x * BPW;
-    const int nb = kp.n - board0 < BPW ? kp.n - board0 : BPW;
-
-    for (int i = tid; i < BPW * FS; i += 256) {
-        const int b = i / FS, k = i - b * FS;
-        fk[k * BPW + b] = b < nb ? kp.feat[(size_t)(board0 + b) * FS + k] : 0.f;
-    }
-    __syncthreads();
 
     // policy heads: Dense(2HW -> P_r) + softmax
     for (int r = 0; r < kp.R; ++r) {
         const int P = kp.P[r], K = 2 * NPOS;
         const float* Wd = kp.pd[r];
-        const float4* f4 = (const float4*)(fk + (size_t)r * 2 * NPOS * BPW);
+        const float* fr = fk + (size_t)r * 2 * NPOS * BPW;
         for (int j = tid; j < P; j += 256) {
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll 8
+            float a[BPW];
+#pragma unroll
+            for (int b = 0; b < BPW; ++b) a[b] = 0.f;
+#pragma unroll 32   // many weight loads in flight: the loop is L2-latency bound
             for (int k = 0; k < K; ++k) {
                 const float w = Wd[(size_t)k * P + j];
-                const float4 f = f4[k];
-                a0 += f.x * w; a1 += f.y * w; a2 += f.z * w; a3 += f.w * w;
+#pragma unroll
+                for (int b = 0; b < BPW; ++b) a[b] += fr[k * BPW + b] * w;
             }
             const float bj = kp.pb[r][j];
-            lg[0 * LMAX + j] = a0 + bj;
-            lg[1 * LMAX + j] = a1 + bj;
-            lg[2 * LMAX + j] = a2 + bj;
-            lg[3 * LMAX + j] = a3 + bj;
+#pragma unroll
+            for (int b = 0; b < BPW; ++b) lg[b * LMAX + j] = a[b] + bj;
         }
         __syncthreads();
         if (wave < nb) {                  // wave b: softmax of board b
@@ -996,10 +999,10 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
             float m = -3.0e38f;
             for (int j = lane; j < P; j += 64) m = fmaxf(m, l[j]);
             m = wave_max(m);
-            float s = 0.f;
-            for (int j = lane; j < P; j += 64) s += __expf(l[j] - m);
-            s = wave_sum(s);
-            const float inv = 1.f / s;
+            float sum = 0.f;
+            for (int j = lane; j < P; j += 64) sum += __expf(l[j] - m);
+            sum = wave_sum(sum);
+            const float inv = 1.f / sum;
             const int board = board0 + b;
             const int sg = find_segment(kp, board);
             float* out = kp.seg[sg].pol[r] + (size_t)(board - kp.seg[sg].row0) * P;
@@ -1011,20 +1014,20 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
     // value head: Dense([GAP F] + HW -> VH) + act, Dense(VH -> V) + softmax
     {
         const int VH = kp.VH, VK = kp.gapF + NPOS;
-        const float4* f4 = (const float4*)(fk + (size_t)2 * kp.R * NPOS * BPW);
+        const float* fv = fk + (size_t)2 * kp.R * NPOS * BPW;
         for (int j = tid; j < VH; j += 256) {
-            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll 8
+            float a[BPW];
+#pragma unroll
+            for (int b = 0; b < BPW; ++b) a[b] = 0.f;
+#pragma unroll 32   // many weight loads in flight: the loop is L2-latency bound
             for (int k = 0; k < VK; ++k) {
                 const float w = kp.vhw[(size_t)k * VH + j];
-                const float4 f = f4[k];
-                a0 += f.x * w; a1 += f.y * w; a2 += f.z * w; a3 += f.w * w;
+#pragma unroll
+                for (int b = 0; b < BPW; ++b) a[b] += fv[k * BPW + b] * w;
             }
             const float bj = kp.vhb[j];
-            lg[0 * LMAX + j] = act_fn(a0 + bj, kp.leaky);
-            lg[1 * LMAX + j] = act_fn(a1 + bj, kp.leaky);
-            lg[2 * LMAX + j] = act_fn(a2 + bj, kp.leaky);
-            lg[3 * LMAX + j] = act_fn(a3 + bj, kp.leaky);
+#pragma unroll
+            for (int b = 0; b < BPW; ++b) lg[b * LMAX + j] = act_fn(a[b] + bj, kp.leaky);
         }
         __syncthreads();
         if (wave < nb) {
@@ -1032,9 +1035,9 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
             const float* hv = lg + b * LMAX;
             float o[4] = {0.f, 0.f, 0.f, 0.f};
             for (int v = 0; v < kp.V; ++v) {
-                float s = 0.f;
-                for (int k = lane; k < VH; k += 64) s += hv[k] * kp.vdw[(size_t)k * kp.V + v];
-                o[v] = wave_sum(s) + kp.vdb[v];
+                float sum = 0.f;
+                for (int k = lane; k < VH; k += 64) sum += hv[k] * kp.vdw[(size_t)k * kp.V + v];
+                o[v] = wave_sum(sum) + kp.vdb[v];
             }
             if (lane == 0) {
                 const int board = board0 + b;
@@ -1045,14 +1048,41 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
                 } else {
                     float m = o[0];
                     for (int v = 1; v < kp.V; ++v) m = fmaxf(m, o[v]);
-                    float e[4], sum = 0.f;
-                    for (int v = 0; v < kp.V; ++v) { e[v] = __expf(o[v] - m); sum += e[v]; }
-                    for (int v = 0; v < kp.V; ++v) out[v] = e[v] / sum;
+                    float e[4], esum = 0.f;
+                    for (int v = 0; v < kp.V; ++v) { e[v] = __expf(o[v] - m); esum += e[v]; }
+                    for (int v = 0; v < kp.V; ++v) out[v] = e[v] / esum;
                 }
             }
         }
     }
-    (void)red;
+}
+
+// LDS of the fused heads (trunk kernels with two activation images): 1x1-conv partials, features,
+// dense outputs
+__host__ __device__ inline int fused_heads_bytes(int npos, int R, int maxP, int VH, int gapF, int nb) {
+    const int FS = (2 * R + 1) * npos + gapF;
+    const int LMAX = maxP > VH ? maxP : VH;
+    return align16(4 * (2 * R + 1) * npos * 4) + align16(FS * nb * 4) + align16(nb * LMAX * 4);
+}
+
+// Separate heads launch (single-image trunk kernels: kHeadBoards boards per workgroup of features
+// from the device scratch).
+#ifdef GZNN_DEFINE_HEADS_KERNEL   // defined in one translation unit (gz_nn.hip)
+__global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
+    constexpr int BPW = kHeadBoards;
+    extern __shared__ __attribute__((aligned(16))) float hs[];
+    const int FS = kp.FS;
+    float* fk = hs;                       // [FS][BPW]
+    float* lg = hs + FS * BPW;            // [BPW][LMAX]
+    const int tid = threadIdx.x;
+    const int board0 = blockIdx.x * BPW;
+    const int nb = kp.n - board0 < BPW ? kp.n - board0 : BPW;
+    for (int i = tid; i < BPW * FS; i += 256) {
+        const int b = i / FS, k = i - b * FS;
+        fk[k * BPW + b] = b < nb ? kp.feat[(size_t)(board0 + b) * FS + k] : 0.f;
+    }
+    __syncthreads();
+    dense_heads<BPW>(kp, fk, lg, board0, nb);
 }
 
 #endif

@@ -46,6 +46,7 @@ struct gz_net {
         int smem = 0;              // dynamic LDS bytes
         int btab_off = 0;          // LDS offset of the bias table
         int se_off = 0;            // LDS offset of the squeeze-excite scratch
+        bool fused_heads = false;  // the dense heads run inside the trunk kernel (no heads_kernel launch)
         int resid_bytes = 0;       // global residual scratch per workgroup
     } small, large;                // launches below / from large_min_rows rows
     int large_min_rows = 1 << 30;
@@ -175,11 +176,15 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     const int npos = d.input_columns * d.input_rows;
     // LDS: two ping-pong activation images per board; the scratch (input staging, heads) aliases
     // the second image set, which holds nothing live at those times.
-    const int scr = trunk_scratch_bytes(npos, d.input_channels, net->K0, d.role_count, net->p2);
+    const int scr_in = trunk_scratch_bytes(npos, d.input_channels, net->K0, d.role_count, net->p2);
     auto trunk = [&](const KernelChoice& c) {
         gz_net::Trunk t;
         t.fn = c.fn;
         t.nb = c.nb;
+        t.fused_heads = !c.single_image;
+        const int scr = t.fused_heads ? std::max(scr_in, fused_heads_bytes(npos, d.role_count, maxP, d.value_hidden_size,
+                                                                           gap_features(d), c.nb))
+                                      : scr_in;
         t.btab_off = c.single_image ? align16(std::max(c.act_bytes, scr))
                                     : c.nb * c.act_bytes + std::max(c.nb * c.act_bytes, scr);
         t.resid_bytes = c.resid_bytes;
@@ -258,6 +263,8 @@ extern "C" void gz_net_destroy(gz_net* net) {
 }
 
 extern "C" size_t gz_net_weight_count(const gz_net* net) { return net ? net->nweights : 0; }
+
+extern "C" int gz_net_heads_fused(const gz_net* net) { return net->large.fused_heads ? 1 : 0; }
 
 extern "C" double gz_net_flops_per_eval(const gz_net* net) {
     const gz_net_desc& d = net->d;   // = NetDesc.flops_per_eval (desc.py)
@@ -578,8 +585,9 @@ static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* se
     void* args[] = {&kp};
     HIPCHK(hipLaunchKernel(t.fn, dim3((n + t.nb - 1) / t.nb), dim3(256), args, t.smem, stream));
     if (mid) HIPCHK(hipEventRecord(mid, stream));
-    HIPCHK(hipLaunchKernel((const void*)&heads_kernel, dim3((n + kHeadBoards - 1) / kHeadBoards), dim3(256), args,
-                           net->heads_smem, stream));
+    if (!t.fused_heads)
+        HIPCHK(hipLaunchKernel((const void*)&heads_kernel, dim3((n + kHeadBoards - 1) / kHeadBoards), dim3(256), args,
+                               net->heads_smem, stream));
     return 0;
 }
 

@@ -118,6 +118,10 @@ int gz_net_wave_rows(const gz_net* net);
 /* Algorithmic FLOPs of one leaf evaluation (2 FLOP/MAC). */
 double gz_net_flops_per_eval(const gz_net* net);
 
+/* 1 when the large (two-board) trunk variant runs the dense policy / value heads itself (two-image
+ * kernels: no separate heads launch), 0 when a separate heads kernel follows it. */
+int gz_net_heads_fused(const gz_net* net);
+
 const char* gz_nn_last_error(void);
 
 /* Diagnostics: with GZ_KERNEL_STAMPS set in the environment, gz_net_forward records per-workgroup
