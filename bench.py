@@ -45,8 +45,13 @@ NUM_CUS = 256
 # separate rocprofv3 --pmc passes, tools/gpu_pmc.sh).  PMC counters cannot be read inside the timed
 # run, so the figure measured for the same kernel is reported with its source.
 TRAFFIC_PER_LAUNCH = {"gznn::trunk_kernel<128, 4, 1, 1, 1>": (14290.1 * 2 + 320.0) * 1024,
-                      "gznn::trunk_kernel<128, 4, 2, 1, 1>": (14722.3 * 2 + 800.0) * 1024}
-TRAFFIC_SOURCE = "profiles/r01k_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 256- and 640-row launches)"
+                      "gznn::trunk_kernel<128, 4, 2, 1, 1>": (14722.3 * 2 + 800.0) * 1024,
+                      "gznn::trunk_kernel<128, 4, 2, 1, 3>": (59483.6 * 2 + 1280.0) * 1024}
+TRAFFIC_SOURCE = {
+    "gznn::trunk_kernel<128, 4, 1, 1, 1>": "profiles/r01k_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 256-row launches)",
+    "gznn::trunk_kernel<128, 4, 2, 1, 1>": "profiles/r01k_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 640-row launches)",
+    "gznn::trunk_kernel<128, 4, 2, 1, 3>": "profiles/r02r_pmc_fp32_1024rows.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+                                           "separate passes, 1024-row launches; FETCH x2 gfx950 correction, 1 KB units)"}
 
 
 def parse():
@@ -423,7 +428,7 @@ def main():
                          "peak_basis": "dense bf16 MFMA %.0f TFLOP/s / %d MFMAs per algorithmic product" % (PEAK_BF16_TFLOPS, p),
                          "traffic": TRAFFIC_PER_LAUNCH.get(dom) if args.config == 2 else None,
                          "traffic_unit": "bytes/launch",
-                         "traffic_source": TRAFFIC_SOURCE if args.config == 2 and dom in TRAFFIC_PER_LAUNCH else None,
+                         "traffic_source": TRAFFIC_SOURCE.get(dom) if args.config == 2 else None,
                          "kernel": dom, "avg_kernel_ms": per_variant[dom]["avg_kernel_ms"] if dom else None,
                          "rows_per_launch": per_variant[dom]["rows_per_launch"] if dom else None,
                          "flop_per_leaf_kernel": kernel_flops, "heads_fused": heads_fused, "variants": per_variant,

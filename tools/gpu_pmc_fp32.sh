@@ -1,0 +1,18 @@
+#!/bin/bash
+# PMC passes (FETCH_SIZE | WRITE_SIZE | SQ counters), each its own rocprofv3 run, on the fp32-accuracy
+# (split) forward at the bench's launch size (1024 rows)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${1:-pmc_fp32}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+KV="$R/tools/kernel_variants.py --configs 2 --batches 1024 --reps 30 --variants default --precision fp32"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 $KV > $OUT/fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 $KV > $OUT/write.log 2>&1 || { echo "write pass failed"; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+    SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $OUT/sq -o sq -- \
+    python3 $KV > $OUT/sq.log 2>&1 || { echo "sq pass failed"; exit 1; }
+python3 $R/tools/pmc_summary.py $(find $OUT -name "*counter_collection.csv") > $OUT/summary.txt
+find $OUT -name "*counter_collection.csv" -size +2M -delete
+cat $OUT/summary.txt
+echo PMC OK
