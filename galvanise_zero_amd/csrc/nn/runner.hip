@@ -47,6 +47,9 @@ struct Pool {
 
 struct Batch {
     hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;
+    hipEvent_t evc = nullptr;        // planes copied to d_planes (copy stream)
+    float* d_planes = nullptr;       // device staging of the batch's planes
+    size_t d_cap = 0;                // rows d_planes holds
     std::vector<int> pools;
     int rows = 0;
 };
@@ -67,6 +70,12 @@ struct gz_runner {
     std::vector<std::thread> threads;
     std::thread launcher;
     hipStream_t stream = nullptr;
+    // Planes go to HBM by DMA on their own stream (hipMemcpyAsync from the pools' pinned buffers),
+    // overlapping the batch in flight, instead of each trunk workgroup gathering its boards over
+    // PCIe when it starts (a burst of ~2.6 MB per wave of workgroups with the MFMAs waiting on it).
+    // GZ_RUNNER_ZERO_COPY=1: the kernel reads the pinned planes directly (the round-1 path).
+    hipStream_t copy_stream = nullptr;
+    bool zero_copy = false;
     Batch batches_ring[2];
 
     std::mutex qm;                   // guards queue
@@ -290,6 +299,36 @@ static void launcher_main(gz_runner* r) {
             for (int j = 0; j < r->num_policies; ++j) segs[k].policies[j] = p.h_pol[j];
             segs[k].values = p.h_val;
         }
+        if (!r->zero_copy) {
+            // this slot's previous batch has retired (two slots, retired in order): its staging
+            // buffer is free
+            const size_t row_floats = (size_t)r->total_size;
+            if (b.d_cap < (size_t)b.rows) {
+                if (b.d_planes) (void)hipFree(b.d_planes);
+                b.d_planes = nullptr;
+                const size_t cap = std::max((size_t)b.rows, (size_t)4096);
+                if (hipMalloc((void**)&b.d_planes, cap * row_floats * 4) != hipSuccess) {
+                    set_failed(r, "device plane staging allocation failed");
+                    return;
+                }
+                b.d_cap = cap;
+            }
+            size_t off = 0;
+            for (gz_segment& sg : segs) {
+                if (sg.rows > 0 &&
+                    hipMemcpyAsync(b.d_planes + off * row_floats, sg.planes, (size_t)sg.rows * row_floats * 4,
+                                   hipMemcpyHostToDevice, r->copy_stream) != hipSuccess) {
+                    set_failed(r, "plane copy failed");
+                    return;
+                }
+                sg.planes = b.d_planes + off * row_floats;
+                off += sg.rows;
+            }
+            if (hipEventRecord(b.evc, r->copy_stream) != hipSuccess || hipStreamWaitEvent(r->stream, b.evc, 0) != hipSuccess) {
+                set_failed(r, "plane copy event failed");
+                return;
+            }
+        }
         if (hipEventRecord(b.ev0, r->stream) != hipSuccess ||
             gz_net_forward_segments_ev(r->net, r->stream, segs.data(), (int)segs.size(), b.evm) != 0 ||
             hipEventRecord(b.ev1, r->stream) != hipSuccess) {
@@ -344,10 +383,16 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
     r->num_values = num_values;
     r->policy_sizes.assign(policy_sizes, policy_sizes + num_policies);
     r->large_min_rows = gz_net_large_min_rows(net);
-    bool ok = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess;
+    bool ok = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&r->copy_stream, hipStreamNonBlocking) == hipSuccess;
+    {
+        const char* e = std::getenv("GZ_RUNNER_ZERO_COPY");
+        r->zero_copy = e != nullptr && e[0] == '1';
+    }
     for (Batch& b : r->batches_ring)
         ok = ok && hipEventCreate(&b.ev0) == hipSuccess && hipEventCreate(&b.evm) == hipSuccess &&
-             hipEventCreateWithFlags(&b.ev1, hipEventBlockingSync) == hipSuccess;
+             hipEventCreateWithFlags(&b.ev1, hipEventBlockingSync) == hipSuccess &&
+             hipEventCreateWithFlags(&b.evc, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         g_err = "stream / event creation failed";
         gz_runner_destroy(r);
@@ -507,12 +552,16 @@ extern "C" void gz_runner_destroy(gz_runner* r) {
         if (p.h_planes) (void)hipHostFree(p.h_planes);
         if (p.h_out) (void)hipHostFree(p.h_out);
     }
+    if (r->copy_stream) (void)hipStreamSynchronize(r->copy_stream);
     for (Batch& b : r->batches_ring) {
         if (b.ev0) (void)hipEventDestroy(b.ev0);
         if (b.ev1) (void)hipEventDestroy(b.ev1);
         if (b.evm) (void)hipEventDestroy(b.evm);
+        if (b.evc) (void)hipEventDestroy(b.evc);
+        if (b.d_planes) (void)hipFree(b.d_planes);
     }
     if (r->stream) (void)hipStreamDestroy(r->stream);
+    if (r->copy_stream) (void)hipStreamDestroy(r->copy_stream);
     gz_unique_states_destroy(r->shared_unique);
     delete r;
 }
