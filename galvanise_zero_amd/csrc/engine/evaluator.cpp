@@ -581,10 +581,17 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
         return chosen;
     }
 
+    PuctNodeChild* cs = node->children();
+    {   // the pass below streams the whole child array: request every line of it up front (the
+        // array is usually cold -- hundreds of games' trees per thread -- and its lines are
+        // independent, so their misses overlap instead of trickling in behind the loop)
+        const char* p0 = reinterpret_cast<const char*>(cs);
+        const char* p1 = reinterpret_cast<const char*>(cs + n);
+        for (const char* q = p0; q < p1; q += 64) __builtin_prefetch(q, 1, 3);
+    }
     SelectScratch& S = t_sel;
     S.reserve(n);
     const int lead = node->lead_role_index;
-    PuctNodeChild* cs = node->children();
     const bool latch = node->visits > 1000 && node->visits < 40000000 && depth == 0;
     const float limit_latch_root = 0.66;
 

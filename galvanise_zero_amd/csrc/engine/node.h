@@ -133,6 +133,7 @@ struct ModelResult {
 class PuctNodeRequest {
 public:
     explicit PuctNodeRequest(PuctNode* node) : node(node) {}
+    const PuctNode* target() const { return node; }
     const uint64_t* getBaseState() const { return node->getBaseState(); }
     void add(float* buf, const GdlBasesTransformer* transformer) const;
     void reply(const ModelResult& result, const GdlBasesTransformer* transformer);

@@ -40,6 +40,7 @@ void NetworkScheduler::evaluate(PuctNodeRequest* request) {
 
     const int idx = (int)requestors.size();
     requestors.push_back(coro_current());
+    request_nodes.push_back(request->target());
     coro_switch_to(main_loop);
 
     // back: predictions for this batch are in predict_done_event, our row is idx
@@ -83,6 +84,18 @@ static void reap(std::vector<Coro*>& all, Coro* g) {
     coro_destroy(g);
 }
 
+void NetworkScheduler::prefetch_reply(int idx) const {
+    const PuctNode* node = request_nodes[idx];
+    const char* a = reinterpret_cast<const char*>(node);
+    const char* b = reinterpret_cast<const char*>(node->children() + node->num_children);
+    for (const char* q = a; q < b; q += 64) __builtin_prefetch(q, 1, 3);
+    const int r = node->lead_role_index > 0 ? node->lead_role_index : 0;
+    const float* pol = predict_done_event->policies[r] + (size_t)idx * transformer->getPolicySize(r);
+    const char* pa = reinterpret_cast<const char*>(pol);
+    const char* pb = reinterpret_cast<const char*>(pol + transformer->getPolicySize(r));
+    for (const char* q = pa; q < pb; q += 64) __builtin_prefetch(q, 0, 3);
+}
+
 // scheduler.cpp:132-205
 void NetworkScheduler::mainLoop() {
     while (true) {
@@ -104,11 +117,17 @@ void NetworkScheduler::mainLoop() {
             coro_switch_to(top);
             GZ_ASSERT(predict_done_event->pred_count == (int)requestors.size());
             if (!requestors.empty()) {
-                for (Coro* req : requestors) {
-                    coro_switch_to(req);
-                    runnables.push_back(req);
+                // replies in request order; the next request's node (header and child array, which
+                // its reply writes) and its policy row are requested while this one replies: they
+                // are cold (hundreds of games per thread) and independent of this reply
+                const int n = (int)requestors.size();
+                for (int i = 0; i < n; ++i) {
+                    if (i + 1 < n) prefetch_reply(i + 1);
+                    coro_switch_to(requestors[i]);
+                    runnables.push_back(requestors[i]);
                 }
                 requestors.clear();
+                request_nodes.clear();
             }
             if (!yielders.empty()) {
                 for (Coro* y : yielders) runnables.push_back(y);

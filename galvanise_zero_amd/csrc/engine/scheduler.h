@@ -51,11 +51,13 @@ public:
 
 private:
     void mainLoop();
+    void prefetch_reply(int idx) const;
 
     const GdlBasesTransformer* transformer;
     const unsigned int batch_size;
 
     std::vector<Coro*> requestors;
+    std::vector<const PuctNode*> request_nodes;   // the node each requestor waits to have replied
     std::vector<Coro*> yielders;
     std::deque<Coro*> runnables;
     std::vector<Coro*> all_coros;
