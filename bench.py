@@ -333,11 +333,11 @@ def main():
          d["kernel_launches"], d["segments"], d["completed_game_evals"], d["trunk_ms"],
          d["large_launches"], d["large_rows"], d["large_trunk_ms"], d["engine_idle_ms"],
          d["no_samples"], d["resigns"], d["aborts"], d["dupes"], d["tree_playouts"],
-         aged["games_completed"], games_per_rank, blob_sum],
+         aged["games_completed"], games_per_rank, blob_sum, d["large_rounds"]],
         elapsed, device="cuda")
     (rows, batches, games, games_s, samples, kms, launches, segments, game_evals, tms,
      l_launches, l_rows, l_tms, idle_ms, no_samples, resigns, aborts, dupes, tree_playouts,
-     aged_games, games_total, blob_sums) = totals
+     aged_games, games_total, blob_sums, l_rounds) = totals
 
     if rank == 0:
         flops = desc.flops_per_eval()
@@ -384,6 +384,11 @@ def main():
             wg = pv["rows_per_launch"] / nb
             cus = min(wg, NUM_CUS)
             rate = wg * wbytes / (pv["avg_kernel_ms"] / 1e3) / cus / 1e9
+            if nb == 2 and pv["launches"] > 0:
+                # workgroup rounds (one trunk workgroup per CU): rows / (rounds x one round's rows)
+                # is how full the launches' last rounds were
+                pv["rounds_per_launch"] = l_rounds / pv["launches"]
+                pv["row_fill"] = (pv["rows_per_launch"] * pv["launches"]) / (l_rounds * nb * NUM_CUS) if l_rounds else None
             pv["l2_weight_stream"] = {"bytes_per_workgroup": wbytes, "workgroups_per_launch": wg,
                                       "achieved_GBps_per_cu": rate, "peak_GBps_per_cu": PEAK_L2_GBPS_PER_CU,
                                       "frac": rate / PEAK_L2_GBPS_PER_CU}

@@ -435,7 +435,8 @@ class GzRunnerStats(ctypes.Structure):
                 ("resigns", ctypes.c_long), ("aborts", ctypes.c_long), ("dupes", ctypes.c_long),
                 ("segments", ctypes.c_long), ("completed_game_evals", ctypes.c_long),
                 ("large_launches", ctypes.c_long), ("large_rows", ctypes.c_long), ("large_trunk_ms", ctypes.c_double),
-                ("engine_idle_ms", ctypes.c_double), ("tree_playouts", ctypes.c_long)]
+                ("engine_idle_ms", ctypes.c_double), ("tree_playouts", ctypes.c_long),
+                ("large_rounds", ctypes.c_long)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

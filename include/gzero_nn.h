@@ -177,6 +177,7 @@ typedef struct gz_runner_stats {
     double large_trunk_ms;
     double engine_idle_ms;       /* summed over engine threads: time with none of the thread's pools ready */
     long tree_playouts;          /* tree playouts of all games (NN-free ones = tree_playouts - rows) */
+    long large_rounds;           /* workgroup rounds of the large launches: sum of ceil(rows / gz_net_wave_rows) */
 } gz_runner_stats;
 
 gz_runner* gz_runner_create(gz_net* net, const struct gz_sm* sm, const struct gz_transformer* t,

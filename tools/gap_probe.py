@@ -26,10 +26,12 @@ def main():
     ap.add_argument("--rows", default="512,1024,1536")
     ap.add_argument("--gaps-us", default="0,300,1000,3000")
     ap.add_argument("--reps", type=int, default=40)
+    ap.add_argument("--weight-seed", type=int, default=3)
+    ap.add_argument("--bias-std", type=float, default=0.1)
     args = ap.parse_args()
     desc = BASELINE_CONFIGS[2]["desc"]
     net = HipNet(desc, 0, args.precision)
-    net.set_weights(to_blob(random_weights(desc, 3, bias_std=0.1)))
+    net.set_weights(to_blob(random_weights(desc, args.weight_seed, bias_std=args.bias_std)))
     stream = torch.cuda.Stream()
     for n in [int(r) for r in args.rows.split(",")]:
         planes = torch.from_numpy(random_planes(desc, n, 9)).pin_memory()
@@ -56,8 +58,8 @@ def main():
             if not gap:
                 torch.cuda.synchronize()
                 ts = [a.elapsed_time(b) for a, b in ts[2:]]
-            print("%s rows %5d gap %5d us: median %.3f ms  min %.3f  max %.3f"
-                  % (args.precision, n, gap, np.median(ts), np.min(ts), np.max(ts)), flush=True)
+            print("w%d/b%.2f %s rows %5d gap %5d us: median %.3f ms  min %.3f  max %.3f"
+                  % (args.weight_seed, args.bias_std, args.precision, n, gap, np.median(ts), np.min(ts), np.max(ts)), flush=True)
     net.close()
 
 
