@@ -366,7 +366,7 @@ def main():
         kernel_flops = desc.flops_per_eval() if heads_fused else desc.flops_trunk()
         per_variant = {}
         for name, (vl, vr, vt) in variants.items():
-            if vl > 0 and vt > 0:
+            if vl > 0 and vr > 0 and vt > 0:
                 wl, wr, wt = whole[name]
                 per_variant[name] = {"launches": vl, "rows_per_launch": vr / vl, "avg_kernel_ms": vt / vl,
                                      "achieved_tflops": kernel_flops * vr / (vt / 1e3) / 1e12,
@@ -382,8 +382,8 @@ def main():
         for name, pv in per_variant.items():
             nb = 2 if name.endswith(", 2, 1, %d>" % p) else 1
             wg = pv["rows_per_launch"] / nb
-            cus = min(wg, NUM_CUS)
-            rate = wg * wbytes / (pv["avg_kernel_ms"] / 1e3) / cus / 1e9
+            cus = max(min(wg, NUM_CUS), 1e-9)
+            rate = wg * wbytes / (max(pv["avg_kernel_ms"], 1e-9) / 1e3) / cus / 1e9
             if nb == 2 and pv["launches"] > 0:
                 # workgroup rounds (one trunk workgroup per CU): rows / (rounds x one round's rows)
                 # is how full the launches' last rounds were

@@ -99,6 +99,11 @@ struct KParams {
 
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
 
+// the dense policy / value heads (defined with heads_kernel below; the two-image trunk kernels call
+// it themselves)
+template <int BPW>
+__device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, float* lg, int board0, int nb);
+
 // The board geometry at run time (kernels are compiled per filter count and position-tile count):
 // p / W as (p * ceil(65536 / W)) >> 16, exact for W <= 32 and p < 1024 (checked on the host).
 constexpr int kMaxPTN = 11;        // position tiles of the largest compiled board (13 x 13)
@@ -643,14 +648,22 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) acc[ct][bb * PT + pt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < (K0 >> 5); ++s) {
-            bf16x8 a[CT], alo[CT];
+        // initial-conv weights one k-step ahead of their MFMAs (each step's fragments would
+        // otherwise wait a full L2 round trip)
+        const int nk0 = K0 >> 5;
+        bf16x8 a[CT], alo[CT];
+        auto load_w0 = [&](int s, bf16x8 (&x)[CT], bf16x8 (&xl)[CT]) {
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
                 const size_t o = ((size_t)(s * F + co_base + 16 * ct + li)) * 32 + 8 * g;
-                a[ct] = *(const bf16x8*)(kp.w0 + o);
-                if constexpr (P2 == 2) alo[ct] = *(const bf16x8*)(kp.w0lo + o);
+                x[ct] = *(const bf16x8*)(kp.w0 + o);
+                if constexpr (P2 == 2) xl[ct] = *(const bf16x8*)(kp.w0lo + o);
             }
+        };
+        load_w0(0, a, alo);
+        for (int s = 0; s < nk0; ++s) {
+            bf16x8 an[CT], alon[CT];
+            if (s + 1 < nk0) load_w0(s + 1, an, alon);
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) {
                 const int p = 16 * pt + li;
@@ -666,6 +679,13 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], bql, c, 0, 0, 0);
                         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[ct], bq, c, 0, 0, 0);
                     }
+                }
+            }
+            if (s + 1 < nk0) {
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) {
+                    a[ct] = an[ct];
+                    if constexpr (P2 == 2) alo[ct] = alon[ct];
                 }
             }
         }
@@ -871,6 +891,20 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     // features in the model's Flatten order go to the scratch for heads_kernel ----------------
     const int HC = 2 * kp.R + 1;
     float* hpart = (float*)SCR;                                  // [4][HC][NPOS]
+    // the heads' 1x1 conv weights of this wave's channels, loaded together once for the NB boards
+    // (two-role games, F <= 128) instead of one dependent global load per conv and board
+    constexpr int kHoistHC = 5;
+    constexpr bool HOIST_WH = !SI && CT <= 2;
+    float4 whv[HOIST_WH ? kHoistHC : 1][CT];
+    if constexpr (HOIST_WH) {
+        if (HC <= kHoistHC) {
+#pragma unroll
+            for (int h = 0; h < kHoistHC; ++h)
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct)
+                    if (h < HC) whv[h][ct] = *(const float4*)(kp.wh + (size_t)h * F + co_base + 16 * ct + 4 * g);
+        }
+    }
     // FUSE (two-image kernels): the features stay in LDS, fk = [FS][NB], and the dense heads run
     // here; single-image kernels write them to the device scratch for heads_kernel
     constexpr bool FUSE = !SI;
@@ -896,24 +930,38 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                         if (co + r < kp.gapF) feat_at(bb, 2 * kp.R * NPOS + co + r) = sm[r] * inv;
             }
         }
-        for (int h = 0; h < HC; ++h) {
-            float wv[CT][4];
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                const float4 w4 = *(const float4*)(kp.wh + (size_t)h * F + co_base + 16 * ct + 4 * g);
-                wv[ct][0] = w4.x; wv[ct][1] = w4.y; wv[ct][2] = w4.z; wv[ct][3] = w4.w;
-            }
+        // one 1x1 head conv (output h) of board bb from the fp32 stream, weights wv
+        auto head_conv = [&](int h, const float4 (&wv)[CT]) {
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) {
                 float s = 0.f;
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) s += acc[ct][bb * PT + pt][r] * wv[ct][r];
+                for (int ct = 0; ct < CT; ++ct) {
+                    const f32x4 a = acc[ct][bb * PT + pt];
+                    s += a[0] * wv[ct].x;
+                    s += a[1] * wv[ct].y;
+                    s += a[2] * wv[ct].z;
+                    s += a[3] * wv[ct].w;
+                }
                 s += __shfl_xor(s, 16, 64);
                 s += __shfl_xor(s, 32, 64);
                 const int p = 16 * pt + li;
                 if (g == 0 && p < NPOS) hpart[(wave * HC + h) * NPOS + p] = s;
+            }
+        };
+        if constexpr (HOIST_WH) {
+            if (HC <= kHoistHC) {
+#pragma unroll
+                for (int h = 0; h < kHoistHC; ++h)
+                    if (h < HC) head_conv(h, whv[h]);
+            }
+        }
+        if (!HOIST_WH || HC > kHoistHC) {
+            for (int h = 0; h < HC; ++h) {
+                float4 wv[CT];
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) wv[ct] = *(const float4*)(kp.wh + (size_t)h * F + co_base + 16 * ct + 4 * g);
+                head_conv(h, wv);
             }
         }
         __syncthreads();

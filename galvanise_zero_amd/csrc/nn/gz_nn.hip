@@ -645,6 +645,7 @@ extern "C" int gz_net_forward(gz_net* net, const float* planes, int n, float* co
         HIPCHK(hipMalloc((void**)&net->d_stamps, (size_t)grid * 8 * sizeof(unsigned long long)));
         net->stamp_cap = grid;
     }
+    if (stamps) HIPCHK(hipMemsetAsync(net->d_stamps, 0, (size_t)grid * 8 * sizeof(unsigned long long), net->stream));
     HIPCHK(hipEventRecord(net->ev0, net->stream));
     net->stamps_on = stamps;
     const int lrc = launch(net, net->stream, d_in, n, d_pol, d_val);
@@ -659,9 +660,16 @@ extern "C" int gz_net_forward(gz_net* net, const float* planes, int n, float* co
     if (stamps) {
         std::vector<unsigned long long> h((size_t)grid * 8);
         HIPCHK(hipMemcpy(h.data(), net->d_stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        // the launch ran ceil(n / NB) workgroups: average over the ones that stamped
         for (int i = 0; i < 8; ++i) net->stamp_avg[i] = 0;
-        for (int b = 0; b < grid; ++b)
-            for (int i = 1; i < 4; ++i) net->stamp_avg[i] += (double)(h[(size_t)b * 8 + i] - h[(size_t)b * 8 + i - 1]) / grid;
+        int wgs = 0;
+        for (int b = 0; b < grid; ++b) {
+            if (h[(size_t)b * 8] == 0 || h[(size_t)b * 8 + 3] == 0) continue;
+            ++wgs;
+            for (int i = 1; i < 4; ++i) net->stamp_avg[i] += (double)(h[(size_t)b * 8 + i] - h[(size_t)b * 8 + i - 1]);
+        }
+        for (int i = 1; i < 4; ++i) net->stamp_avg[i] = wgs ? net->stamp_avg[i] / wgs : 0.0;
+        net->stamp_avg[0] = wgs;
     }
     return 0;
 }

@@ -228,6 +228,10 @@ static void launcher_main(gz_runner* r) {
                 p.rows_done = p.rows;
                 p.state.store(kEngine, std::memory_order_release);
             }
+            // every counter of a launch is taken when it retires, so a stats snapshot never holds a
+            // launch without its rows
+            r->launches.fetch_add(1, std::memory_order_relaxed);
+            r->segments.fetch_add((long)b.pools.size(), std::memory_order_relaxed);
             r->rows.fetch_add(b.rows, std::memory_order_relaxed);
             r->batches.fetch_add(1, std::memory_order_relaxed);
             inflight.pop_front();
@@ -343,6 +347,15 @@ static void launcher_main(gz_runner* r) {
             }
         }
         if (b.pools.empty()) continue;
+        if (b.rows == 0) {   // pools with nothing to evaluate: hand them back without a launch
+            for (int i : b.pools) {
+                Pool& p = r->pools[i];
+                p.rows_done = p.rows;
+                p.state.store(kEngine, std::memory_order_release);
+            }
+            r->cv.notify_all();
+            continue;
+        }
         segs.assign(b.pools.size(), gz_segment{});
         for (size_t k = 0; k < b.pools.size(); ++k) {
             Pool& p = r->pools[b.pools[k]];
@@ -388,8 +401,6 @@ static void launcher_main(gz_runner* r) {
             set_failed(r, std::string("launch failed: ") + gz_nn_last_error());
             return;
         }
-        r->launches.fetch_add(1, std::memory_order_relaxed);
-        r->segments.fetch_add((long)segs.size(), std::memory_order_relaxed);
         inflight.push_back(next_slot);
         next_slot ^= 1;
     }

@@ -125,8 +125,9 @@ int gz_net_heads_fused(const gz_net* net);
 const char* gz_nn_last_error(void);
 
 /* Diagnostics: with GZ_KERNEL_STAMPS set in the environment, gz_net_forward records per-workgroup
- * s_memtime stamps at phase boundaries; out8[1..5] = mean cycles of (input + initial conv,
- * residual trunk, head 1x1 convs, policy dense + softmax, value head) of the last call. */
+ * s_memtime stamps at phase boundaries; out8[0] = workgroups averaged, out8[1..3] = their mean
+ * cycles of (input + initial conv, residual trunk, head 1x1 convs + features + fused dense heads)
+ * in the last call. */
 int gz_net_stamp_avg(const gz_net* net, double* out8);
 
 /* ---- native self-play driver (runner.hip) ----------------------------------------------------
