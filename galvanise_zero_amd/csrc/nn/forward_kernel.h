@@ -387,10 +387,12 @@ __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, P
                 __builtin_amdgcn_sched_group_barrier(0x008, CT * (P2 == 2 ? 3 : 1), 0);   // MFMA
                 __builtin_amdgcn_sched_group_barrier(0x100, P2, 0);                       // DS read
             }
-            // k-step boundary: nothing crosses it, so the next k-step's B reads stay one k-step
-            // ahead of their MFMAs (double buffer) and scheduling regions stay one k-step long
-            __builtin_amdgcn_sched_barrier(0);
         }
+        // k-step boundary: nothing crosses it, so the next k-step's B reads stay one k-step ahead
+        // of their MFMAs (double buffer) and scheduling regions stay one k-step long (also in the
+        // single-image kernels: without it their 9-tap branch-free conv became one region whose
+        // schedule put each B read next to its use)
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
