@@ -281,7 +281,7 @@ class GzPoolStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_long) for n in (
         "games_started", "games_completed", "games_with_samples", "samples", "no_samples", "dupes",
         "resigns", "false_positive_resigns0", "false_positive_resigns1", "early_run_to_ends",
-        "aborts_game_length", "evaluations", "polls", "completed_game_evals", "tree_playouts")]
+        "aborts_game_length", "evaluations", "polls", "completed_game_evals", "tree_playouts", "transpositions")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

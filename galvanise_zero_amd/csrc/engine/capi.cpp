@@ -113,6 +113,7 @@ static void to_stats(const PoolStats& s, gz_pool_stats* o) {
     o->polls = s.polls;
     o->completed_game_evals = s.completed_game_evals;
     o->tree_playouts = s.tree_playouts;
+    o->transpositions = s.transpositions;
 }
 
 // ---- JSON of samples (sampleToDict, supervisor_impl.cpp:75-118) ---------------------------------
@@ -482,6 +483,7 @@ extern "C" int gz_pool_clear_unique_states(gz_pool* p) {
 extern "C" int gz_pool_get_stats(gz_pool* p, gz_pool_stats* out) {
     PoolStats s = p->impl->getStats();
     s.tree_playouts = p->impl->treePlayouts();
+    s.transpositions = p->impl->transpositions();
     to_stats(s, out);
     return 0;
 }

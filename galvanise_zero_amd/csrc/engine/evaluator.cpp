@@ -63,6 +63,18 @@ void PuctEvaluator::removeNode(PuctNode* node) {
     number_of_nodes--;
 }
 
+// A transposed node (lookup_transpositions) is referenced by several parents, but its mirror entry
+// (in_parent) and its parent pointer name the first one only.  When that edge is dropped and the
+// node survives through another parent, both are cleared: syncParent() would otherwise write into
+// the freed parent's child array, and createSample / the planes' previous state would read the
+// freed parent (the reference reads it there: evaluator.cpp:102-140 never updates `parent`).
+static inline void detachEdge(PuctNodeChild* edge, PuctNode* node) {
+    if (node->ref_count > 0 && node->in_parent == edge) {
+        node->in_parent = nullptr;
+        node->parent = nullptr;
+    }
+}
+
 void PuctEvaluator::releaseNodes(PuctNode* current) {
     const int role_count = sm->roleCount();
     for (int ii = 0; ii < current->num_children; ii++) {
@@ -75,6 +87,8 @@ void PuctEvaluator::releaseNodes(PuctNode* current) {
             if (next_node->ref_count == 0) {
                 releaseNodes(next_node);
                 garbage.push_back(next_node);
+            } else {
+                detachEdge(child, next_node);
             }
         }
     }
@@ -135,6 +149,7 @@ PuctNode* PuctEvaluator::expandChild(PuctNode* parent, PuctNodeChild* child) {
     if (child->to_node != nullptr) {
         child->to_node->ref_count++;
         stats.num_transpositions_attached++;
+        total_transpositions++;
         mirror_ok = false;   // a node with two parents: only one of them holds its mirror
     } else {
         child->unselectable = true;
@@ -1474,6 +1489,8 @@ PuctNode* PuctEvaluator::fastApplyMove(const PuctNodeChild* next) {
             if (next_node->ref_count == 0) {
                 releaseNodes(next_node);
                 garbage.push_back(next_node);
+            } else {
+                detachEdge(c, next_node);
             }
         }
     }

@@ -80,6 +80,7 @@ public:
     const PlayoutStats& getStats() const { return stats; }
     long totalEvaluations() const { return total_evaluations; }
     long totalTreePlayouts() const { return total_tree_playouts; }
+    long totalTranspositions() const { return total_transpositions; }
 
 private:
     void removeNode(PuctNode*);
@@ -151,6 +152,7 @@ private:
     long node_allocated_memory = 0;
     long total_evaluations = 0;
     long total_tree_playouts = 0;   // diagnostics: NN-free playouts = tree playouts - evaluations
+    long total_transpositions = 0;  // diagnostics: edges attached to an existing node (lookup_transpositions)
     bool do_playouts = false;
     bool mirror_ok = true;   // every node has one parent: the child mirrors (node.h) are exact
     PlayoutStats stats;

@@ -110,6 +110,7 @@ struct PoolStats {
     long polls = 0;
     long completed_game_evals = 0; // NN evaluations consumed by the games counted in games_completed
     long tree_playouts = 0;        // tree playouts of every game of the pool (filled by treePlayouts())
+    long transpositions = 0;       // transposition edges attached (filled by transpositions())
 };
 
 class SelfPlayManager {
@@ -136,6 +137,11 @@ public:
     long treePlayouts() const {
         long n = 0;
         for (const PuctEvaluator* pe : evaluators) n += pe->totalTreePlayouts();
+        return n;
+    }
+    long transpositions() const {
+        long n = 0;
+        for (const PuctEvaluator* pe : evaluators) n += pe->totalTranspositions();
         return n;
     }
 

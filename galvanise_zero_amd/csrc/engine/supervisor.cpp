@@ -163,6 +163,7 @@ PoolStats Supervisor::stats() {
         s.polls += p.polls;
         s.completed_game_evals += p.completed_game_evals;
         s.tree_playouts += m->treePlayouts();
+        s.transpositions += m->transpositions();
     }
     return s;
 }

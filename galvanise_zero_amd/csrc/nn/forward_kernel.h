@@ -144,7 +144,10 @@ struct Geo {
     static constexpr bool WRAP = CPR == 16 && P2 == 2;
     static constexpr int HALF = WRAP ? 256 : ((CPR + 14) * 16 + 255) & ~255;   // one part's row
     static constexpr int ROWS = P2 * HALF;           // LDS row stride: hi part, then lo part
-    static constexpr int ACT_BYTES = (NPOS + 1) * ROWS;           // + one all-zero row (at row kp.npos)
+    // + one all-zero row (row kp.npos: every off-board 3x3 neighbour reads it) and one scratch row
+    // (row kp.npos + 1: the epilogues of a partial last position tile store their off-board lanes
+    // there instead of branching around the store)
+    static constexpr int ACT_BYTES = (NPOS + 2) * ROWS;
     // k-steps per ring stage and the ring's VGPR budget: F = 256 (4 co tiles per wave, 16 weight
     // VGPRs per k-step) streams single k-steps through a 64-VGPR ring so the accumulators, the
     // residual and the B fragments still fit the 512 registers of a wave without spilling
@@ -196,8 +199,10 @@ __host__ __device__ inline int bias_table_bytes(int F, int B) { return align16((
 // squeeze-excite scratch: per board the channel means [F] and the compressed units [kMaxSE]
 __host__ __device__ inline int se_scratch_bytes(int F, int NB) { return NB * (F + kMaxSE) * 4; }
 
+// ReLU / LeakyReLU(0.03) as max(v, alpha v) (alpha < 1): a multiply and a max, no compare / select
+// (a negative v gives -0.0 under ReLU instead of +0.0; every later use is unchanged by the sign)
 __device__ __forceinline__ float act_fn(float v, int leaky) {
-    return v > 0.f ? v : (leaky ? 0.03f * v : 0.f);
+    return fmaxf(v, (leaky ? 0.03f : 0.f) * v);
 }
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
@@ -210,9 +215,11 @@ __device__ __forceinline__ float bf16_lo(float x) { return x - (float)(__bf16)x;
 template <int F, int PTN, int P = 1>
 __device__ __forceinline__ void store_act(char* X, int p, int co, f32x4 v, int npos) {
     using G = Geo<F, PTN, 1, P>;
-    if (p < npos) {
-        const int chunk = G::WRAP ? (((co >> 3) + swz(p)) & 15) : ((co >> 3) + swz(p));
-        char* a = X + p * G::ROWS + (chunk << 4) + (co & 7) * 2;
+    {
+        // off-board lanes of a partial last tile write the scratch row (a select, not a branch)
+        const int q = p < npos ? p : npos + 1;
+        const int chunk = G::WRAP ? (((co >> 3) + swz(q)) & 15) : ((co >> 3) + swz(q));
+        char* a = X + q * G::ROWS + (chunk << 4) + (co & 7) * 2;
         uint2 u;
         u.x = pack2(v[0], v[1]);
         u.y = pack2(v[2], v[3]);

@@ -41,6 +41,10 @@ KernelChoice variants(int v, int precision) {
         if constexpr (F <= 128 && PTN <= 4) {
             if constexpr (2 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024) {
                 if (v == 11) return kernel_for<F, PTN, 1, 1, 3, V2>();
+                // one board per workgroup, two workgroups per CU (two waves per SIMD: one
+                // workgroup's epilogues and barriers overlap the other's MFMAs)
+                if constexpr (PTN == 4 && 4 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024)
+                    if (v == 12) return kernel_for<F, PTN, 1, 2, 3, V2>();
                 // two boards per workgroup (F = 128: 256-byte wrapped rows, hi + lo in 512 bytes)
                 if constexpr (Geo<F, PTN, 1, 3>::WRAP && 4 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024)
                     if (v == 21) return kernel_for<F, PTN, 2, 1, 3, V2>();

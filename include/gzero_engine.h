@@ -96,6 +96,7 @@ typedef struct gz_pool_stats {
     long polls;
     long completed_game_evals;   /* NN evaluations consumed by the completed games */
     long tree_playouts;          /* tree playouts (treePlayout calls), NN-free ones included */
+    long transpositions;         /* edges attached to an existing node (lookup_transpositions) */
 } gz_pool_stats;
 
 const char* gz_engine_last_error(void);

@@ -1,0 +1,122 @@
+"""Diagnostic builds of the F = 128, 8x8 split trunk kernel (not product code): copies csrc/nn to
+/tmp, applies one source patch per experiment, and builds libgz_nn.so (only the F = 128 / PT = 4
+instantiations; the other filter counts are stubbed) into tools/kexp/lib_<name>/ next to a copy of
+libgz_engine.so.  Timing on the GPU box: GZ_LIB_DIR=tools/kexp/lib_<name> python tools/kernel_variants.py ...
+
+  base         unpatched (same-box reference)
+  nostore      the residual epilogues compute but do not write the next LDS image (epilogue ds_writes)
+  l1weights    every weight-ring stage reads stage 0's fragments (weights from L1 instead of L2)
+  nobarrier    no workgroup barrier after the residual epilogues (results wrong; barrier cost)
+  noaddr       every tap reads the centre tap's B addresses (no per-tap address arithmetic)
+  noreads      no B-fragment LDS reads after each conv's first k-step
+  a+b          both patches
+Usage: python tools/kexp/build.py base nostore ...
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+SRC = os.path.join(ROOT, "galvanise_zero_amd", "csrc", "nn")
+
+STUB = r'''
+#include "trunk_variants.h"
+namespace gznn {
+KernelChoice trunk_variant_f128(int pt, int v, int precision) {
+    if (pt == 4) return variants<128, 4>(v, precision);
+    return KernelChoice{};
+}
+KernelChoice trunk_variant_f64(int, int, int) { return KernelChoice{}; }
+KernelChoice trunk_variant_f256(int, int, int) { return KernelChoice{}; }
+KernelChoice trunk_variant_f64_v2(int, int, int) { return KernelChoice{}; }
+KernelChoice trunk_variant_f128_v2(int, int, int) { return KernelChoice{}; }
+}
+'''
+
+
+def patch(name, text):  # noqa: C901
+    def rep(old, new, count=1):
+        nonlocal text
+        assert text.count(old) >= count, (name, old)
+        text = text.replace(old, new)
+    if name == "base":
+        pass
+    elif name == "nostore":
+        rep("        *(uint2*)a = u;\n", "        if (npos < 0) *(uint2*)a = u;\n")
+        rep("            *(uint2*)(a + G::HALF) = l;\n", "            if (npos < 0) *(uint2*)(a + G::HALF) = l;\n")
+    elif name == "l1weights":
+        rep("    const int s = gs < gmax ? gs : gmax;\n", "    const int s = (gs < gmax ? gs : gmax) & 0;\n")
+    elif name == "nobarrier":
+        # the two barriers closing the v1 residual epilogues (two-image kernels)
+        rep("                store_act<F, PTN, P>(X1 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);\n"
+            "            }\n        }\n        __syncthreads();\n",
+            "                store_act<F, PTN, P>(X1 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);\n"
+            "            }\n        }\n")
+        rep("                store_act<F, PTN, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);\n"
+            "            }\n        }\n        __syncthreads();\n    }\n",
+            "                store_act<F, PTN, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);\n"
+            "            }\n        }\n    }\n")
+    elif name == "noaddr":
+        rep("    const int dy = tap / 3 - 1, dx = tap % 3 - 1;\n", "    const int dy = 0, dx = 0;\n")
+        rep("    const bool ok = (bd.tapmask[pt] >> tap) & 1;\n", "    const bool ok = (bd.tapmask[pt] >> 4) & 1;\n")
+    elif name == "noreads":
+        rep("        if (j + 1 < 9 * KC) {                  // B fragments of the next k-step (double buffer)\n",
+            "        if (false) {\n")
+        rep("                acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[j & 1][t][0], acc[ct][t], 0, 0, 0);\n",
+            "                acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[0][t][0], acc[ct][t], 0, 0, 0);\n")
+        rep("                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[j & 1][t][1], acc[ct][t], 0, 0, 0);\n",
+            "                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[0][t][1], acc[ct][t], 0, 0, 0);\n")
+        rep("                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[j & 1][t][0], acc[ct][t], 0, 0, 0);\n",
+            "                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[0][t][0], acc[ct][t], 0, 0, 0);\n")
+    elif "+" in name:
+        for part in name.split("+"):
+            text = patch(part, text)
+    else:
+        raise SystemExit("unknown experiment " + name)
+    return text
+
+
+def build(name):
+    work = "/tmp/kexp_" + name
+    shutil.rmtree(work, ignore_errors=True)
+    shutil.copytree(SRC, os.path.join(work, "nn"))
+    os.makedirs(os.path.join(work, "include"), exist_ok=True)
+    for h in ("gzero_nn.h", "gzero_engine.h"):
+        shutil.copy(os.path.join(ROOT, "include", h), os.path.join(work, "include", h))
+    nn = os.path.join(work, "nn")
+    # the sources include ../../../include/...: mirror that depth
+    for f in os.listdir(nn):
+        p = os.path.join(nn, f)
+        t = open(p).read().replace("../../../include/", "../include/")
+        if f == "forward_kernel.h":
+            t = patch(name, t)
+        open(p, "w").write(t)
+    open(os.path.join(nn, "trunk_exp.hip"), "w").write(STUB)
+    out = os.path.join(ROOT, "tools", "kexp", "lib_" + name)
+    os.makedirs(out, exist_ok=True)
+    eng = os.path.join(out, "libgz_engine.so")
+    if not os.path.lexists(eng):
+        os.symlink("../../../galvanise_zero_amd/lib/libgz_engine.so", eng)
+    flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-parameter"]
+    objs = []
+    procs = []
+    for tu in ("gz_nn.hip", "runner.hip", "trunk_exp.hip"):
+        o = os.path.join(work, tu + ".o")
+        objs.append(o)
+        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc"] + flags + ["-c", "-o", o, os.path.join(nn, tu)]))
+    for p in procs:
+        assert p.wait() == 0, name
+    subprocess.check_call(["/opt/rocm/bin/hipcc"] + flags + ["-shared", "-o", os.path.join(out, "libgz_nn.so")] + objs +
+                          ["-L" + out, "-lgz_engine", "-Wl,-rpath,$ORIGIN"])
+    print("built", out)
+
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or ["base"]
+    procs = [subprocess.Popen([sys.executable, __file__, "--one", n]) for n in names] if "--one" not in sys.argv else None
+    if procs is None:
+        build(sys.argv[2])
+    else:
+        rc = [p.wait() for p in procs]
+        sys.exit(max(rc))
