@@ -75,7 +75,10 @@ def parse():
                     help="trunk arithmetic: fp32 = split hi/lo bf16 operands, three MFMAs per product "
                          "(fp32-class accuracy, the reference runs fp32 TF; default where the kernel "
                          "has it, F <= 128); bf16 = bf16 operands (default for the F = 256 configs)")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=30.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=60.0)
+    ap.add_argument("--opening-seconds", type=float, default=30.0,
+                    help="also report the GPU leg's rate over the first seconds of aging (the opening phase the "
+                         "CPU baseline measures)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--min-launch-rows", type=int, default=1024,
@@ -140,7 +143,9 @@ def cpu_baseline(seconds, evals, mode, batch, config=2):
     sm, transformer, desc = setup_game(config)
     cores = cpu_share()
     torch.set_num_threads(cores)
-    workers = max(1, cores // 8)   # the network, not the tree search, is the CPU cost here
+    # the tree search gets every core but one (C++ worker threads, each with its two pools, as the
+    # GPU leg's engine threads); the network's torch threads share the same cores
+    workers = max(1, cores - 1)
     model = TorchCPUNet(desc, random_weights(desc, 7921))
 
     class NN(object):
@@ -150,6 +155,7 @@ def cpu_baseline(seconds, evals, mode, batch, config=2):
             return model
 
     sup = cppinterface.Supervisor(sm, NN(), batch_size=batch, seed=1, per_pool_unique_states=True)
+    t_start = time.time()
     sup.start_self_play(selfplay_conf(mode, evals), workers)
     t_end = time.time() + min(5.0, seconds / 4)          # warm the pools (first batches, torch init)
     while time.time() < t_end:
@@ -161,7 +167,8 @@ def cpu_baseline(seconds, evals, mode, batch, config=2):
     el = time.time() - t0
     rows = sup.total_predictions - rows0
     return {"value": rows / el, "unit": "leaf-evals/s", "cores": cores, "kind": "port",
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "worker_threads": workers, "torch_threads": cores,
+            "phase": "opening: %.0f-%.0f s after the start of self-play" % (t0 - t_start, t0 - t_start + el),
             "sample": "%.1f s of %s self-play from the initial position (%d evals/move, %s mode): the reference's "
                       "worker-thread design (%d C++ worker threads x 2 pools x %d games, Supervisor.poll loop) with "
                       "a float32 torch-CPU network on %d threads" % (el, sm.game, evals, mode, workers, batch, cores)}
@@ -296,10 +303,15 @@ def main():
 
     runner.start()
     # ---- aging: until the population has turned over (or the time limit) ----------------------
+    # the first --opening-seconds of it are also reported as the opening-phase rate (the phase the
+    # CPU baseline runs in)
     age_target = args.age_games * games_per_rank
+    opening = None
     while args.age_seconds > 0:
         st = runner.stats()
         el = time.perf_counter() - t_start
+        if opening is None and el >= args.opening_seconds:
+            opening = {"seconds": el, "rows": st["rows"], "leaf_evals_per_s": st["rows"] / el}
         if st["games_completed"] >= age_target or el >= args.age_seconds:
             break
         runner.wait_rows(st["rows"] + (1 << 18), timeout_s=600)
@@ -333,13 +345,19 @@ def main():
          d["kernel_launches"], d["segments"], d["completed_game_evals"], d["trunk_ms"],
          d["large_launches"], d["large_rows"], d["large_trunk_ms"], d["engine_idle_ms"],
          d["no_samples"], d["resigns"], d["aborts"], d["dupes"], d["tree_playouts"],
-         aged["games_completed"], games_per_rank, blob_sum, d["large_rounds"]],
+         aged["games_completed"], games_per_rank, blob_sum, d["large_rounds"], d["split_launches"]],
         elapsed, device="cuda")
     (rows, batches, games, games_s, samples, kms, launches, segments, game_evals, tms,
      l_launches, l_rows, l_tms, idle_ms, no_samples, resigns, aborts, dupes, tree_playouts,
-     aged_games, games_total, blob_sums, l_rounds) = totals
+     aged_games, games_total, blob_sums, l_rounds, split_launches) = totals
 
     if rank == 0:
+        # host budget: leaf evaluations one engine thread sustains (this window) against what the
+        # GPU's forward could absorb at its measured per-row time; fewer engine threads than that
+        # leave the GPU waiting on the host
+        per_thread = rows / T / (threads * world) if T > 0 else float("nan")
+        gpu_capacity = rows / (kms / 1e3) / world if kms > 0 else float("nan")
+        threads_needed = int(-(-gpu_capacity // per_thread)) if per_thread > 0 else None
         flops = desc.flops_per_eval()
         avg_fwd_s = (kms / launches) / 1e3 if launches else float("nan")
         rows_per_launch = rows / launches if launches else float("nan")
@@ -415,13 +433,15 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32 (split bf16 hi+lo operands, 3 MFMAs per product, fp32 accumulate)" if p == 3 else "bf16",
+            "dtype": "bf16x3 split (hi+lo bf16 operands, ~16-bit significand, 3 MFMAs per product, fp32 accumulate)"
+                     if p == 3 else "bf16",
             "data": "synthetic: self-play from the initial position, random-init weights (no .h5 in reference)",
             "config": {"workload": "%s self-play (BASELINE configs[%d]), v1 %dx%d net, %d evals/move (%s mode), "
                                    "eval batch %d" % (sm.game, args.config - 1, desc.residual_layers,
                                                       desc.cnn_filter_size, evals, args.mode, args.batch),
                        "step": "%d leaf evaluations per rank" % args.step_rows,
                        "games_per_gpu": games_per_rank, "threads_per_gpu": threads, "cpus_per_gpu": cpus,
+                       "cpus_per_rank": cpus,
                        "pools_per_thread": args.pools, "eval_batch": args.batch,
                        "launch_batching": {"min_rows": args.min_launch_rows, "max_wait_us": args.max_launch_wait_us},
                        "parallelism": "games sharded dp%d" % world,
@@ -443,6 +463,15 @@ def main():
                          "forward_tflops": flops * rows_per_launch / avg_fwd_s / 1e12,
                          "flop_per_leaf": flops, "aggregate_tflops": flops * rows / T / 1e12},
             "gpu_busy_frac": (kms / 1e3) / (T * world) if T > 0 else None,
+            "split_launches": split_launches,
+            "host_budget": {"leaf_evals_per_s_per_engine_thread": per_thread,
+                            "gpu_forward_capacity_leaf_evals_per_s": gpu_capacity,
+                            "engine_threads_per_gpu": threads, "engine_threads_needed_per_gpu": threads_needed,
+                            "warning": ("host-bound: %d engine threads per GPU, about %d would keep the GPU busy"
+                                        % (threads, threads_needed)) if threads_needed and threads < threads_needed
+                                       else None},
+            "opening": {"leaf_evals_per_s_rank0": opening["leaf_evals_per_s"], "seconds": opening["seconds"]}
+                       if opening else None,
             "engine_idle_frac": (idle_ms / 1e3) / (T * world * threads) if T > 0 else None,
             "host_peak_rss_gb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6,
         }

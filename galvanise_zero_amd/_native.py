@@ -102,6 +102,7 @@ def nn_lib():
         lib.gz_net_flops_per_eval.argtypes = [ctypes.c_void_p]
         lib.gz_net_heads_fused.restype = ctypes.c_int
         lib.gz_net_heads_fused.argtypes = [ctypes.c_void_p]
+        lib.gz_net_set_output_logits.argtypes = [ctypes.c_void_p, ctypes.c_int]
         lib.gz_nn_last_error.restype = ctypes.c_char_p
         lib._gz_typed = True
     return lib
@@ -203,6 +204,10 @@ class HipNet(object):
 
     def last_kernel_ms(self):
         return self.lib.gz_net_last_kernel_ms(self.handle)
+
+    def set_output_logits(self, on=True):
+        """Diagnostics: later forwards return the heads' pre-activation outputs (logits)."""
+        self._check(self.lib.gz_net_set_output_logits(self.handle, int(bool(on))), "gz_net_set_output_logits")
 
     def stamp_avg(self):
         out = (ctypes.c_double * 8)()
@@ -436,7 +441,7 @@ class GzRunnerStats(ctypes.Structure):
                 ("segments", ctypes.c_long), ("completed_game_evals", ctypes.c_long),
                 ("large_launches", ctypes.c_long), ("large_rows", ctypes.c_long), ("large_trunk_ms", ctypes.c_double),
                 ("engine_idle_ms", ctypes.c_double), ("tree_playouts", ctypes.c_long),
-                ("large_rounds", ctypes.c_long)]
+                ("large_rounds", ctypes.c_long), ("split_launches", ctypes.c_long)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -458,5 +463,8 @@ def runner_lib():
         lib.gz_runner_destroy.argtypes = [_VP]
         lib.gz_runner_last_error.restype = ctypes.c_char_p
         lib.gz_runner_clear_unique_states.argtypes = [_VP]
+        lib.gz_runner_update_network.argtypes = [_VP, _VP, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_double]
+        lib.gz_runner_roll_info.argtypes = [_VP, ctypes.POINTER(ctypes.c_long), ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_long)]
         lib._gz_runner_typed = True
     return lib

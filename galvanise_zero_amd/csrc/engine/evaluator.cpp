@@ -7,15 +7,53 @@
 #include "transformer.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <random>
 
 namespace gz {
+
+// log((1 + visits + 19652) / 19652) in float, as the reference computes it (evaluator.cpp:1300-1307):
+// every selection at every node evaluates it (a root spin run once per playout, at consecutive
+// visit counts), so the values for visits < 2^26 are tabulated, 64K at a time on first use, with
+// the same expression and the same libm call (identical bits); larger counts call logf directly.
+static float puct_log_direct(uint32_t visits) {
+    const float cpuct_base_id = 19652.0f;
+    return std::log((1 + visits + cpuct_base_id) / cpuct_base_id);
+}
+
+namespace {
+constexpr int kPuctLogBlockBits = 16, kPuctLogBlocks = 1024;   // visits < 2^26
+std::atomic<float*> g_puct_log[kPuctLogBlocks];
+std::mutex g_puct_log_mu;
+
+__attribute__((noinline)) float* puct_log_block(uint32_t b) {
+    std::lock_guard<std::mutex> lk(g_puct_log_mu);
+    float* t = g_puct_log[b].load(std::memory_order_acquire);
+    if (t == nullptr) {
+        t = new float[1u << kPuctLogBlockBits];
+        const uint32_t v0 = b << kPuctLogBlockBits;
+        for (uint32_t i = 0; i < (1u << kPuctLogBlockBits); ++i) t[i] = puct_log_direct(v0 + i);
+        g_puct_log[b].store(t, std::memory_order_release);
+    }
+    return t;
+}
+}  // namespace
+
+static inline float puct_log(uint32_t visits) {
+    const uint32_t b = visits >> kPuctLogBlockBits;
+    if (b >= (uint32_t)kPuctLogBlocks) return puct_log_direct(visits);
+    float* t = g_puct_log[b].load(std::memory_order_acquire);
+    if (__builtin_expect(t == nullptr, 0)) t = puct_log_block(b);
+    return t[visits & ((1u << kPuctLogBlockBits) - 1)];
+}
+
 
 #define GZ_ASSERT(cond)                                                                     \
     do {                                                                                    \
@@ -1123,9 +1161,8 @@ bool PuctEvaluator::spinBuild() {
     // the FPU prior of unexpanded children: the top-visits child is a win (chooseTopVisits returns
     // the first win), so prior = win score - fpu * sqrt(...) <= win score
     const double prior_bound = (double)win_score;
-    const float cpuct_base_id = 19652.0f;
     auto pc_at = [&](uint32_t v) {
-        float p = std::log((1 + v + cpuct_base_id) / cpuct_base_id);
+        float p = puct_log(v);
         p += conf->puct_constant_root;
         return p;
     };
@@ -1700,9 +1737,8 @@ void PuctEvaluator::setDirichletNoise(PuctNode* node) {
 
 // evaluator.cpp:1300-1307
 void PuctEvaluator::setPuctConstant(PuctNode* node, int depth) const {
-    const float cpuct_base_id = 19652.0f;
     const float puct_constant = depth == 0 ? conf->puct_constant_root : conf->puct_constant;
-    node->puct_constant = std::log((1 + node->visits + cpuct_base_id) / cpuct_base_id);
+    node->puct_constant = puct_log(node->visits);
     node->puct_constant += puct_constant;
 }
 

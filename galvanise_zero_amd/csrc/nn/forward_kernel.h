@@ -86,6 +86,7 @@ struct KParams {
     int C, K0, B, R, VH, V, leaky, flatten_nchw, maxP, npos;
     int H, W, wmagic;        // board rows / columns; wmagic = ceil(65536 / W) (Board::div)
     int value_sigmoid;       // legacy model files: independent sigmoid per value output
+    int logits;              // diagnostics (gz_net_set_output_logits): write pre-softmax / pre-sigmoid outputs
     int v2;                  // pre-activation blocks: stream s += conv2(act(BN(conv1(act(BN(s)))))) [* SE gate]
     int k0taps;              // initial conv taps: 9 (3x3) or 1 (1x1, v2)
     int init_act;            // activation after the initial conv (0: v2 files with a bare initial conv)
@@ -992,11 +993,12 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         }
         __syncthreads();    // hpart is reused by the next board
     }
+    GZ_STAMP(3);
     if constexpr (FUSE) {
         const int nb = kp.n - board0 < NB ? kp.n - board0 : NB;
         dense_heads<NB>(kp, fk, lg, board0, nb);
     }
-    GZ_STAMP(3);
+    GZ_STAMP(4);
 #undef GZ_STAMP
 }
 
@@ -1063,7 +1065,11 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
             const int board = board0 + b;
             const int sg = find_segment(kp, board);
             float* out = kp.seg[sg].pol[r] + (size_t)(board - kp.seg[sg].row0) * P;
-            for (int j = lane; j < P; j += 64) out[j] = __expf(l[j] - m) * inv;
+            if (kp.logits) {
+                for (int j = lane; j < P; j += 64) out[j] = l[j];
+            } else {
+                for (int j = lane; j < P; j += 64) out[j] = __expf(l[j] - m) * inv;
+            }
         }
         __syncthreads();
     }
@@ -1100,7 +1106,9 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
                 const int board = board0 + b;
                 const int sg = find_segment(kp, board);
                 float* out = kp.seg[sg].val + (size_t)(board - kp.seg[sg].row0) * kp.V;
-                if (kp.value_sigmoid) {
+                if (kp.logits) {
+                    for (int v = 0; v < kp.V; ++v) out[v] = o[v];
+                } else if (kp.value_sigmoid) {
                     for (int v = 0; v < kp.V; ++v) out[v] = 1.f / (1.f + __expf(-o[v]));
                 } else {
                     float m = o[0];

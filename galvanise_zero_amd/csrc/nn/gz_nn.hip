@@ -664,11 +664,11 @@ extern "C" int gz_net_forward(gz_net* net, const float* planes, int n, float* co
         for (int i = 0; i < 8; ++i) net->stamp_avg[i] = 0;
         int wgs = 0;
         for (int b = 0; b < grid; ++b) {
-            if (h[(size_t)b * 8] == 0 || h[(size_t)b * 8 + 3] == 0) continue;
+            if (h[(size_t)b * 8] == 0 || h[(size_t)b * 8 + 4] == 0) continue;
             ++wgs;
-            for (int i = 1; i < 4; ++i) net->stamp_avg[i] += (double)(h[(size_t)b * 8 + i] - h[(size_t)b * 8 + i - 1]);
+            for (int i = 1; i < 5; ++i) net->stamp_avg[i] += (double)(h[(size_t)b * 8 + i] - h[(size_t)b * 8 + i - 1]);
         }
-        for (int i = 1; i < 4; ++i) net->stamp_avg[i] = wgs ? net->stamp_avg[i] / wgs : 0.0;
+        for (int i = 1; i < 5; ++i) net->stamp_avg[i] = wgs ? net->stamp_avg[i] / wgs : 0.0;
         net->stamp_avg[0] = wgs;
     }
     return 0;
@@ -680,6 +680,13 @@ extern "C" int gz_net_stamp_avg(const gz_net* net, double* out8) {
 }
 
 extern "C" float gz_net_last_kernel_ms(const gz_net* net) { return net ? net->last_ms : 0.f; }
+
+extern "C" int gz_net_set_output_logits(gz_net* net, int on) {
+    if (!net) return fail("null net");
+    std::lock_guard<std::mutex> wl(net->wmu);
+    net->kp.logits = on ? 1 : 0;
+    return 0;
+}
 
 extern "C" int gz_net_large_min_rows(const gz_net* net) { return net ? net->large_min_rows : 0; }
 

@@ -2,14 +2,16 @@
 // Python poll loop (cppinterface.py:78-144) + worker threads (supervisor.cpp:79-99, 196-245).
 //
 // T engine threads each own P game pools (SelfPlayManager via the engine C-ABI).  A pool's
-// coroutines write its planes straight into the pool's pinned host buffer; the pool is then handed
-// to ONE launcher thread, which merges every pool waiting at that moment (up to GZ_MAX_SEGMENTS) into
-// a single segmented launch of the fused forward: the kernel gathers each pool's planes from host
-// memory and scatters the policies / values back into the pool's pinned output buffers, so there
-// are no staging copies and no per-pool launches.  While the GPU runs one merged batch, the next
-// accumulates (at most two batches in flight on one stream), so batch size adapts to load: under
-// GPU pressure the launches grow, which is where the kernel is most efficient.  The engine thread
-// meanwhile advances its other pools (the reference's two-managers-per-thread ping-pong, P-way).
+// coroutines write its planes into the pool's pinned host buffer; the pool is then queued for ONE
+// launcher thread, which composes launches from the queue (whole workgroup rounds, splitting a
+// pool's batch between two launches when that fills the last round: see Compose), DMAs each
+// launch's planes to a per-slot HBM staging buffer on a copy stream, and issues one segmented
+// launch of the fused forward (trunk + dense heads in one kernel for the two-image kernels), which
+// writes policies / values straight back into the pools' pinned output buffers.  At most two
+// launches are in flight on the launch stream, so the next batch accumulates while the GPU runs
+// one.  The engine thread meanwhile advances its other pools (the reference's
+// two-managers-per-thread ping-pong, P-way).  GZ_RUNNER_ZERO_COPY=1: the kernel reads the pinned
+// planes itself (no staging copy; round 1).
 #include "../../../include/gzero_engine.h"
 #include "../../../include/gzero_nn.h"
 
@@ -39,10 +41,24 @@ struct Pool {
     float* h_out = nullptr;          // pinned: policies then values, written by the kernel
     std::vector<float*> h_pol;
     float* h_val = nullptr;
-    int rows = 0;                    // rows submitted in the current launch
+    int rows = 0;                    // rows of the pool's current batch (set when queued)
     int rows_done = 0;               // rows whose predictions are in h_out (engine side)
+    int sub = 0;                     // rows of the current batch already in a launch (launcher only)
     std::chrono::steady_clock::time_point queued_at;   // set under qm when queued
     std::atomic<int> state{kEngine};
+    long launched = 0;               // batches whose rows have all been launched (launcher only)
+    long queued_batches = 0;         // batches the engine thread has queued (engine only)
+    // generation roll with per-pool filters: clear this pool's duplicate filter just before its
+    // engine thread delivers batch `clear_at` (its first batch on the new network); -1: none
+    std::atomic<long> clear_at{-1};
+};
+
+// A launch is a list of parts: rows [row0, row0 + rows) of a pool's batch.  A pool's batch may be
+// split over two launches (exact-round composition below); `last` marks the part whose retirement
+// completes the pool's batch (launches on one stream retire in order).
+struct Part {
+    int pool, row0, rows;
+    bool last;
 };
 
 struct Batch {
@@ -50,9 +66,14 @@ struct Batch {
     hipEvent_t evc = nullptr;        // planes copied to d_planes (copy stream)
     float* d_planes = nullptr;       // device staging of the batch's planes
     size_t d_cap = 0;                // rows d_planes holds
-    std::vector<int> pools;
+    std::vector<Part> parts;
     int rows = 0;
 };
+
+// Launch composition: kSplit (default) launches whole workgroup rounds, splitting the last pool's
+// batch; kSubset (round 2) the subset of whole pools that fills its rounds best; kLegacy (round 1)
+// a queue prefix trimmed to whole rounds.  GZ_RUNNER_COMPOSE=split|subset|legacy.
+enum Compose : int { kSplit = 0, kSubset = 1, kLegacy = 2 };
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
 
@@ -76,7 +97,7 @@ struct gz_runner {
     // GZ_RUNNER_ZERO_COPY=1: the kernel reads the pinned planes directly (the round-1 path).
     hipStream_t copy_stream = nullptr;
     bool zero_copy = false;
-    bool legacy_trim = false;        // GZ_RUNNER_LEGACY_TRIM=1: trim launches to exact whole waves only
+    Compose compose = kSplit;
     Batch batches_ring[2];
 
     std::mutex qm;                   // guards queue
@@ -89,6 +110,7 @@ struct gz_runner {
     std::atomic<long> engine_idle_us{0};   // summed over engine threads: no pool of the thread ready
     // launches that ran the multi-board trunk variant (rows >= gz_net_large_min_rows)
     std::atomic<long> large_launches{0}, large_rows{0}, large_trunk_us{0}, large_rounds{0};
+    std::atomic<long> split_launches{0};   // launches holding part of a pool's batch (kSplit)
     int wave_rows = 0;
     int large_min_rows = 1 << 30;
     std::mutex m;
@@ -100,6 +122,17 @@ struct gz_runner {
     gz_unique_states* shared_unique = nullptr;   // per_pool_unique_states == 0: one filter for all pools
     std::atomic<int> live_pools{0};  // pools whose main loop is running (not kDead)
     bool started = false;
+    // generation roll (gz_runner_update_network): applied by the launcher between launches, when no
+    // pool's batch is split, so every batch runs on one network
+    std::mutex roll_m;
+    std::condition_variable roll_cv;
+    std::atomic<int> roll_state{0};  // 0 none, 1 pending, 2 applied, -1 failed
+    const float* roll_blob = nullptr;
+    size_t roll_count = 0;
+    int roll_device = 0, roll_clear = 0;
+    std::string roll_err;
+    std::vector<long> roll_batches;  // per pool: batches launched on the previous network
+    long roll_launches = 0;          // launches issued on the previous network
 };
 
 static void set_failed(gz_runner* r, const std::string& msg) {
@@ -128,6 +161,14 @@ static void engine_main(gz_runner* r, int tid) {
         for (int i : mine) {
             Pool& p = r->pools[i];
             if (p.state.load(std::memory_order_acquire) != kEngine) continue;
+            {
+                // this poll delivers batch queued_batches - 1 (none on the first poll)
+                const long ca = p.clear_at.load(std::memory_order_acquire);
+                if (ca >= 0 && p.queued_batches > 0 && p.queued_batches - 1 == ca) {
+                    if (gz_pool_clear_unique_states(p.pool) != 0) set_failed(r, "clear_unique_states failed");
+                    p.clear_at.store(-1, std::memory_order_release);
+                }
+            }
             const int n = gz_pool_poll(p.pool, p.rows_done);
             if (r->cfg.keep_samples) {
                 long cnt = 0;
@@ -154,9 +195,11 @@ static void engine_main(gz_runner* r, int tid) {
                 continue;
             }
             p.rows = n;
+            p.queued_batches++;
             p.state.store(kQueued, std::memory_order_release);
             {
                 std::lock_guard<std::mutex> lk(r->qm);
+                r->pools[i].sub = 0;
                 r->pools[i].queued_at = std::chrono::steady_clock::now();
                 r->queue.push_back(i);
             }
@@ -182,6 +225,34 @@ static void engine_main(gz_runner* r, int tid) {
     }
 }
 
+// ---- generation roll ----------------------------------------------------------------------------
+// The reference swaps the network between poll loops (worker.py:138-160, Supervisor.update_nn
+// cppinterface.py:146-147) and clears the duplicate filter (supervisor_impl.cpp:138-144); here the
+// launcher swaps it between two launches.  gz_net_set_weights waits for the launches in flight
+// (which finish on the previous image) before freeing it.
+static void apply_roll(gz_runner* r, long launches_issued) {
+    const int rc = r->roll_device ? gz_net_set_weights_device(r->net, r->roll_blob, r->roll_count)
+                                  : gz_net_set_weights(r->net, r->roll_blob, r->roll_count);
+    int rc2 = 0;
+    if (rc == 0 && r->roll_clear) {
+        if (r->shared_unique) {
+            rc2 = gz_unique_states_clear(r->shared_unique);   // one filter for every pool: now
+        } else {
+            // each pool's own filter: at the pool's first batch on the new network (deterministic)
+            for (size_t i = 0; i < r->pools.size(); ++i) r->pools[i].clear_at.store(r->roll_batches[i], std::memory_order_release);
+        }
+    }
+    std::lock_guard<std::mutex> lk(r->roll_m);
+    r->roll_launches = launches_issued;
+    if (rc != 0 || rc2 != 0) {
+        r->roll_err = rc != 0 ? std::string("gz_net_set_weights: ") + gz_nn_last_error() : std::string("clear_unique_states failed");
+        r->roll_state = -1;
+    } else {
+        r->roll_state = 2;
+    }
+    r->roll_cv.notify_all();
+}
+
 // ---- launcher thread --------------------------------------------------------------------------
 static void launcher_main(gz_runner* r) {
     if (hipSetDevice(r->cfg.device) != hipSuccess) {
@@ -199,6 +270,7 @@ static void launcher_main(gz_runner* r) {
     const auto max_wait = std::chrono::microseconds(r->cfg.max_launch_wait_us > 0 ? r->cfg.max_launch_wait_us : 0);
     std::deque<int> inflight;        // indices into batches_ring, oldest first
     int next_slot = 0;
+    long launches_issued = 0;
     std::vector<gz_segment> segs;
     while (true) {
         // retire finished batches (in order: one stream)
@@ -223,15 +295,17 @@ static void launcher_main(gz_runner* r) {
                         r->large_rounds.fetch_add((b.rows + r->wave_rows - 1) / r->wave_rows, std::memory_order_relaxed);
                 }
             }
-            for (int i : b.pools) {
-                Pool& p = r->pools[i];
+            for (const Part& pt : b.parts) {
+                if (!pt.last) continue;
+                Pool& p = r->pools[pt.pool];
                 p.rows_done = p.rows;
                 p.state.store(kEngine, std::memory_order_release);
             }
             // every counter of a launch is taken when it retires, so a stats snapshot never holds a
             // launch without its rows
             r->launches.fetch_add(1, std::memory_order_relaxed);
-            r->segments.fetch_add((long)b.pools.size(), std::memory_order_relaxed);
+            r->segments.fetch_add((long)b.parts.size(), std::memory_order_relaxed);
+            if (b.parts.front().row0 > 0 || !b.parts.back().last) r->split_launches.fetch_add(1, std::memory_order_relaxed);
             r->rows.fetch_add(b.rows, std::memory_order_relaxed);
             r->batches.fetch_add(1, std::memory_order_relaxed);
             inflight.pop_front();
@@ -248,9 +322,21 @@ static void launcher_main(gz_runner* r) {
             (void)hipEventSynchronize(r->batches_ring[inflight.front()].ev1);
             continue;
         }
-        // gather every waiting pool into one segmented launch
+        if (r->roll_state.load(std::memory_order_acquire) == 1) {
+            bool split_pending;
+            {
+                std::lock_guard<std::mutex> lk(r->qm);
+                split_pending = !r->queue.empty() && r->pools[r->queue.front()].sub > 0;
+                if (!split_pending) {
+                    r->roll_batches.resize(r->pools.size());
+                    for (size_t i = 0; i < r->pools.size(); ++i) r->roll_batches[i] = r->pools[i].launched;
+                }
+            }
+            if (!split_pending) apply_roll(r, launches_issued);
+        }
+        // gather waiting pools into one segmented launch
         Batch& b = r->batches_ring[next_slot];
-        b.pools.clear();
+        b.parts.clear();
         b.rows = 0;
         {
             std::unique_lock<std::mutex> lk(r->qm);
@@ -260,14 +346,17 @@ static void launcher_main(gz_runner* r) {
                 else
                     r->qcv.wait_for(lk, std::chrono::microseconds(30));
             }
-            if (min_rows > 0 && !r->queue.empty()) {
-                int queued = 0;
-                for (int i : r->queue) queued += r->pools[i].rows;
-                int inflight_pools = 0;
-                for (int k : inflight) inflight_pools += (int)r->batches_ring[k].pools.size();
-                // no more rows can arrive while every live pool is queued or in flight
-                const bool all_waiting =
-                    (int)r->queue.size() + inflight_pools >= r->live_pools.load(std::memory_order_relaxed);
+            if (r->queue.empty()) continue;
+            int queued = 0;                   // rows waiting (a split pool's remainder included)
+            for (int i : r->queue) queued += r->pools[i].rows - r->pools[i].sub;
+            // no more rows can arrive while no live pool is with its engine thread
+            bool all_waiting = true;
+            for (const Pool& p : r->pools)
+                if (p.state.load(std::memory_order_acquire) == kEngine) {
+                    all_waiting = false;
+                    break;
+                }
+            if (min_rows > 0) {
                 const auto deadline = r->pools[r->queue.front()].queued_at + max_wait;
                 if (queued < min_rows && !all_waiting && (int)r->queue.size() < GZ_MAX_SEGMENTS &&
                     std::chrono::steady_clock::now() < deadline) {
@@ -277,93 +366,120 @@ static void launcher_main(gz_runner* r) {
                     continue;
                 }
             }
-            while (!r->queue.empty() && (int)b.pools.size() < GZ_MAX_SEGMENTS) {
-                const int i = r->queue.front();
-                if (!b.pools.empty() && b.rows + r->pools[i].rows > max_rows) break;
-                r->queue.pop_front();
-                b.pools.push_back(i);
-                b.rows += r->pools[i].rows;
-            }
-            // Whole waves of workgroups: the two-boards-per-workgroup trunk holds one workgroup per
-            // CU (LDS), so a launch of 513-1023 rows takes as long as 1024 (measured: 640 rows
-            // 0.22 ms, 1024 rows 0.23 ms, 512 rows 0.13 ms).  Beyond one wave, launch a multiple of
-            // wave_rows and leave the remaining pools queued for the next launch.
-            if (wave_rows > 0 && b.rows > wave_rows) {
-                if (r->legacy_trim) {
-                    const int target = (b.rows / wave_rows) * wave_rows;
-                    while (b.pools.size() > 1 && b.rows > target && b.rows - r->pools[b.pools.back()].rows >= target) {
-                        b.rows -= r->pools[b.pools.back()].rows;
-                        r->queue.push_front(b.pools.back());
-                        b.pools.pop_back();
+            if (r->compose == kSplit) {
+                // Whole workgroup rounds: the two-boards-per-workgroup trunk runs one workgroup
+                // per CU (LDS), so a launch costs ceil(rows / wave_rows) rounds and a partial last
+                // round idles CUs (pools hold ~215 rows in the steady state, so whole pools rarely
+                // add up to whole rounds).  Launch the largest multiple of wave_rows that is
+                // queued, splitting the last pool's batch; its remainder stays at the queue front
+                // (re-stamped, so it waits for more rows like a newly queued pool).  Fewer rows
+                // than one round, or a queue nothing can join (all_waiting), launch whole.
+                int target = std::min(queued, max_rows);
+                // (a pending generation roll waits for a launch that splits no pool)
+                if (wave_rows > 0 && target > wave_rows && !all_waiting && r->roll_state.load() != 1)
+                    target = (target / wave_rows) * wave_rows;
+                while (!r->queue.empty() && b.rows < target && (int)b.parts.size() < GZ_MAX_SEGMENTS) {
+                    const int i = r->queue.front();
+                    Pool& p = r->pools[i];
+                    const int take = std::min(p.rows - p.sub, target - b.rows);
+                    const bool last = p.sub + take == p.rows;
+                    b.parts.push_back(Part{i, p.sub, take, last});
+                    b.rows += take;
+                    p.sub += take;
+                    if (last) {
+                        r->queue.pop_front();
+                        p.launched++;
+                    } else {
+                        p.queued_at = std::chrono::steady_clock::now();
                     }
-                } else {
-                    // Pools rarely hold exactly 256 rows (games between moves, finished games), so
-                    // whole waves are rarely reachable by a queue prefix (the legacy rule filled
-                    // 69 % of its last rounds in the bench, 3.0 rounds per 1,065-row launch).
-                    // Choose the subset of the gathered pools -- always with the oldest -- whose
-                    // rows fill their workgroup rounds best (0/1 subset sums over <= 32 pools),
-                    // preferring more rounds within 2 % of the best fill; the rest go back to the
-                    // queue front in order.
-                    const int n = (int)b.pools.size();
-                    std::vector<int> rows(n);
-                    for (int k = 0; k < n; ++k) rows[k] = r->pools[b.pools[k]].rows;
-                    const int total = b.rows;
-                    std::vector<int> from(total + 1, -1);   // item that first reached a sum
-                    from[rows[0]] = 0;
-                    for (int k = 1; k < n; ++k)
-                        for (int sum = total; sum >= rows[k]; --sum)
-                            if (from[sum] < 0 && from[sum - rows[k]] >= 0 && sum - rows[k] >= rows[0]) from[sum] = k;
-                    const int max_r = (total + wave_rows - 1) / wave_rows;
-                    std::vector<int> best_sum(max_r + 1, 0);
-                    double best_fill = 0.0;
-                    for (int sum = rows[0]; sum <= total; ++sum)
-                        if (from[sum] >= 0) {
-                            const int rr = (sum + wave_rows - 1) / wave_rows;
-                            best_sum[rr] = sum;     // ascending: the largest reachable sum of rr rounds
+                }
+            } else {
+                std::vector<int> pools;
+                while (!r->queue.empty() && (int)pools.size() < GZ_MAX_SEGMENTS) {
+                    const int i = r->queue.front();
+                    if (!pools.empty() && b.rows + r->pools[i].rows > max_rows) break;
+                    r->queue.pop_front();
+                    pools.push_back(i);
+                    b.rows += r->pools[i].rows;
+                }
+                if (wave_rows > 0 && b.rows > wave_rows) {
+                    if (r->compose == kLegacy) {
+                        // round 1: trim a queue prefix to exact whole waves
+                        const int target = (b.rows / wave_rows) * wave_rows;
+                        while (pools.size() > 1 && b.rows > target && b.rows - r->pools[pools.back()].rows >= target) {
+                            b.rows -= r->pools[pools.back()].rows;
+                            r->queue.push_front(pools.back());
+                            pools.pop_back();
                         }
-                    for (int rr = 1; rr <= max_r; ++rr)
-                        if (best_sum[rr] > 0) best_fill = std::max(best_fill, (double)best_sum[rr] / ((double)rr * wave_rows));
-                    int pick = 0;
-                    for (int rr = max_r; rr >= 1; --rr)
-                        if (best_sum[rr] > 0 && (double)best_sum[rr] / ((double)rr * wave_rows) >= best_fill - 0.02) {
-                            pick = best_sum[rr];
-                            break;
+                    } else {
+                        // round 2: the subset of the gathered pools -- always with the oldest --
+                        // whose rows fill their workgroup rounds best (0/1 subset sums over <= 32
+                        // pools), preferring more rounds within 2 % of the best fill; the rest go
+                        // back to the queue front in order
+                        const int n = (int)pools.size();
+                        std::vector<int> rows(n);
+                        for (int k = 0; k < n; ++k) rows[k] = r->pools[pools[k]].rows;
+                        const int total = b.rows;
+                        std::vector<int> from(total + 1, -1);   // item that first reached a sum
+                        from[rows[0]] = 0;
+                        for (int k = 1; k < n; ++k)
+                            for (int sum = total; sum >= rows[k]; --sum)
+                                if (from[sum] < 0 && from[sum - rows[k]] >= 0 && sum - rows[k] >= rows[0]) from[sum] = k;
+                        const int max_r = (total + wave_rows - 1) / wave_rows;
+                        std::vector<int> best_sum(max_r + 1, 0);
+                        double best_fill = 0.0;
+                        for (int sum = rows[0]; sum <= total; ++sum)
+                            if (from[sum] >= 0) best_sum[(sum + wave_rows - 1) / wave_rows] = sum;
+                        for (int rr = 1; rr <= max_r; ++rr)
+                            if (best_sum[rr] > 0) best_fill = std::max(best_fill, (double)best_sum[rr] / ((double)rr * wave_rows));
+                        int pick = 0;
+                        for (int rr = max_r; rr >= 1; --rr)
+                            if (best_sum[rr] > 0 && (double)best_sum[rr] / ((double)rr * wave_rows) >= best_fill - 0.02) {
+                                pick = best_sum[rr];
+                                break;
+                            }
+                        if (pick > 0 && pick < total) {
+                            std::vector<char> chosen(n, 0);
+                            for (int sum = pick; sum > 0;) {
+                                const int k = from[sum];
+                                chosen[k] = 1;
+                                if (k == 0) break;
+                                sum -= rows[k];
+                            }
+                            std::vector<int> keep, back;
+                            for (int k = 0; k < n; ++k) (chosen[k] ? keep : back).push_back(pools[k]);
+                            for (auto it = back.rbegin(); it != back.rend(); ++it) r->queue.push_front(*it);
+                            pools = keep;
+                            b.rows = pick;
                         }
-                    if (pick > 0 && pick < total) {
-                        std::vector<char> chosen(n, 0);
-                        for (int sum = pick; sum > 0;) {
-                            const int k = from[sum];
-                            chosen[k] = 1;
-                            if (k == 0) break;
-                            sum -= rows[k];
-                        }
-                        std::vector<int> keep, back;
-                        for (int k = 0; k < n; ++k) (chosen[k] ? keep : back).push_back(b.pools[k]);
-                        for (auto it = back.rbegin(); it != back.rend(); ++it) r->queue.push_front(*it);
-                        b.pools = keep;
-                        b.rows = pick;
                     }
+                }
+                for (int i : pools) {
+                    r->pools[i].sub = r->pools[i].rows;
+                    r->pools[i].launched++;
+                    b.parts.push_back(Part{i, 0, r->pools[i].rows, true});
                 }
             }
         }
-        if (b.pools.empty()) continue;
+        if (b.parts.empty()) continue;
         if (b.rows == 0) {   // pools with nothing to evaluate: hand them back without a launch
-            for (int i : b.pools) {
-                Pool& p = r->pools[i];
+            for (const Part& pt : b.parts) {
+                Pool& p = r->pools[pt.pool];
                 p.rows_done = p.rows;
                 p.state.store(kEngine, std::memory_order_release);
             }
             r->cv.notify_all();
             continue;
         }
-        segs.assign(b.pools.size(), gz_segment{});
-        for (size_t k = 0; k < b.pools.size(); ++k) {
-            Pool& p = r->pools[b.pools[k]];
+        segs.assign(b.parts.size(), gz_segment{});
+        for (size_t k = 0; k < b.parts.size(); ++k) {
+            const Part& pt = b.parts[k];
+            Pool& p = r->pools[pt.pool];
             p.state.store(kInFlight, std::memory_order_relaxed);
-            segs[k].rows = p.rows;
-            segs[k].planes = p.h_planes;
-            for (int j = 0; j < r->num_policies; ++j) segs[k].policies[j] = p.h_pol[j];
-            segs[k].values = p.h_val;
+            segs[k].rows = pt.rows;
+            segs[k].planes = p.h_planes + (size_t)pt.row0 * r->total_size;
+            for (int j = 0; j < r->num_policies; ++j) segs[k].policies[j] = p.h_pol[j] + (size_t)pt.row0 * r->policy_sizes[j];
+            segs[k].values = p.h_val + (size_t)pt.row0 * r->num_values;
         }
         if (!r->zero_copy) {
             // this slot's previous batch has retired (two slots, retired in order): its staging
@@ -403,6 +519,7 @@ static void launcher_main(gz_runner* r) {
         }
         inflight.push_back(next_slot);
         next_slot ^= 1;
+        ++launches_issued;
     }
 }
 
@@ -454,7 +571,11 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
         const char* e = std::getenv("GZ_RUNNER_ZERO_COPY");
         r->zero_copy = e != nullptr && e[0] == '1';
         const char* t = std::getenv("GZ_RUNNER_LEGACY_TRIM");
-        r->legacy_trim = t != nullptr && t[0] == '1';
+        if (t != nullptr && t[0] == '1') r->compose = kLegacy;
+        if (const char* c = std::getenv("GZ_RUNNER_COMPOSE")) {
+            const std::string m(c);
+            r->compose = m == "subset" ? kSubset : m == "legacy" ? kLegacy : kSplit;
+        }
     }
     for (Batch& b : r->batches_ring)
         ok = ok && hipEventCreate(&b.ev0) == hipSuccess && hipEventCreate(&b.evm) == hipSuccess &&
@@ -578,6 +699,7 @@ extern "C" int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out) {
     out->large_rows = r->large_rows.load();
     out->large_trunk_ms = r->large_trunk_us.load() / 1000.0;
     out->large_rounds = r->large_rounds.load();
+    out->split_launches = r->split_launches.load();
     out->kernel_launches = r->launches.load();
     out->samples = r->samples_taken.load();
     out->segments = r->segments.load();
@@ -644,5 +766,70 @@ extern "C" int gz_runner_clear_unique_states(gz_runner* r) {
             g_err = gz_engine_last_error();
             return -1;
         }
+    return 0;
+}
+
+// Generation roll on a live runner: the launcher applies the new weights between two launches
+// (no pool batch runs on two networks) and, if asked, clears the duplicate filters; blocks until
+// applied.  Before start / after stop the weights are set directly.
+extern "C" int gz_runner_update_network(gz_runner* r, const float* blob, size_t count, int device_blob,
+                                        int clear_unique_states, double timeout_s) {
+    if (!r || !blob) {
+        g_err = "null argument";
+        return -1;
+    }
+    const bool live = r->started && r->launcher.joinable() && !r->stop.load();
+    if (!live) {
+        const int rc = device_blob ? gz_net_set_weights_device(r->net, blob, count) : gz_net_set_weights(r->net, blob, count);
+        if (rc != 0) {
+            g_err = gz_nn_last_error();
+            return -1;
+        }
+        r->roll_batches.assign(r->pools.size(), 0);
+        for (size_t i = 0; i < r->pools.size(); ++i) r->roll_batches[i] = r->pools[i].launched;
+        r->roll_launches = r->launches.load();
+        if (clear_unique_states && gz_runner_clear_unique_states(r) != 0) return -1;
+        return 0;
+    }
+    std::unique_lock<std::mutex> lk(r->roll_m);
+    if (r->roll_state.load() == 1) {
+        g_err = "a generation roll is already pending";
+        return -1;
+    }
+    r->roll_blob = blob;
+    r->roll_count = count;
+    r->roll_device = device_blob;
+    r->roll_clear = clear_unique_states;
+    r->roll_state = 1;
+    r->qcv.notify_all();
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r->roll_state.load() == 1) {
+        r->roll_cv.wait_for(lk, std::chrono::milliseconds(2));
+        if (r->failed.load()) {
+            g_err = r->fail_msg;
+            return -1;
+        }
+        if (timeout_s > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+            g_err = "timeout waiting for the launcher to apply the generation roll";
+            return -2;
+        }
+    }
+    r->roll_blob = nullptr;
+    if (r->roll_state.load() < 0) {
+        g_err = r->roll_err;
+        r->roll_state = 0;
+        return -1;
+    }
+    r->roll_state = 0;
+    return 0;
+}
+
+// After gz_runner_update_network: per pool, the batches launched on the previous network (the
+// pool's batches 0 .. pool_batches[i]-1 ran on it, the later ones on the new one), and the launches
+// issued before the swap.
+extern "C" int gz_runner_roll_info(gz_runner* r, long* pool_batches, int npools, long* launches_before) {
+    if (!r) return -1;
+    for (int i = 0; i < npools && i < (int)r->roll_batches.size(); ++i) pool_batches[i] = r->roll_batches[i];
+    if (launches_before) *launches_before = r->roll_launches;
     return 0;
 }

@@ -4,6 +4,8 @@ distributed/worker.py:191).  Pools, coroutines, planes and NN launches are all n
 import ctypes
 import json
 
+import numpy as np
+
 from . import _native, cppinterface
 
 
@@ -43,6 +45,26 @@ class SelfPlayRunner(object):
         (worker.py:160)."""
         if self.lib.gz_runner_clear_unique_states(self.handle) != 0:
             raise RuntimeError("gz_runner_clear_unique_states: %s" % self.lib.gz_runner_last_error().decode())
+
+    def update_network(self, blob=None, device_ptr=None, count=None, clear_unique_states=True, timeout_s=120.0):
+        """Generation roll on the live runner (worker.py:138-160: update_nn + clear_unique_states):
+        the launcher swaps in the new weights between two launches, so every pool batch runs on one
+        network.  blob: host float32 weight blob, or device_ptr + count (e.g. after an RCCL
+        broadcast).  Returns {"pool_batches": [batches of each pool launched on the previous
+        network], "launches_before": launches issued before the swap}."""
+        if blob is not None:
+            blob = np.ascontiguousarray(blob, dtype=np.float32)
+            ptr, n, dev = blob.ctypes.data, blob.size, 0
+        else:
+            ptr, n, dev = device_ptr, count, 1
+        rc = self.lib.gz_runner_update_network(self.handle, ctypes.c_void_p(ptr), n, dev, int(bool(clear_unique_states)),
+                                               timeout_s)
+        if rc != 0:
+            raise RuntimeError("gz_runner_update_network (%d): %s" % (rc, self.lib.gz_runner_last_error().decode()))
+        pb = (ctypes.c_long * self.num_pools)()
+        lb = ctypes.c_long()
+        self.lib.gz_runner_roll_info(self.handle, pb, self.num_pools, ctypes.byref(lb))
+        return {"pool_batches": list(pb), "launches_before": lb.value}
 
     def wait_batches(self, total, timeout_s=600.0):
         rc = self.lib.gz_runner_wait_batches(self.handle, total, timeout_s)

@@ -104,6 +104,11 @@ int gz_net_forward(gz_net* net, const float* planes, int n,
 int gz_net_forward_device(gz_net* net, void* stream, const float* d_planes, int n,
                           float* const* d_policies, float* d_values);
 
+/* Diagnostics: on != 0 makes later forwards write the heads' pre-activation outputs (policy logits
+ * before the softmax, value logits before the softmax / sigmoid) instead of probabilities, so parity
+ * tests can compare nets whose softmaxes saturate. */
+int gz_net_set_output_logits(gz_net* net, int on);
+
 /* Device time (ms) of the last gz_net_forward (both launches), measured with HIP events on its stream. */
 float gz_net_last_kernel_ms(const gz_net* net);
 
@@ -125,8 +130,8 @@ int gz_net_heads_fused(const gz_net* net);
 const char* gz_nn_last_error(void);
 
 /* Diagnostics: with GZ_KERNEL_STAMPS set in the environment, gz_net_forward records per-workgroup
- * s_memtime stamps at phase boundaries; out8[0] = workgroups averaged, out8[1..3] = their mean
- * cycles of (input + initial conv, residual trunk, head 1x1 convs + features + fused dense heads)
+ * s_memtime stamps at phase boundaries; out8[0] = workgroups averaged, out8[1..4] = their mean
+ * cycles of (input + initial conv, residual trunk, head 1x1 convs + features, fused dense heads)
  * in the last call. */
 int gz_net_stamp_avg(const gz_net* net, double* out8);
 
@@ -179,6 +184,7 @@ typedef struct gz_runner_stats {
     double engine_idle_ms;       /* summed over engine threads: time with none of the thread's pools ready */
     long tree_playouts;          /* tree playouts of all games (NN-free ones = tree_playouts - rows) */
     long large_rounds;           /* workgroup rounds of the large launches: sum of ceil(rows / gz_net_wave_rows) */
+    long split_launches;         /* launches holding part of a pool's batch (exact-round composition) */
 } gz_runner_stats;
 
 gz_runner* gz_runner_create(gz_net* net, const struct gz_sm* sm, const struct gz_transformer* t,
@@ -196,6 +202,15 @@ char* gz_runner_fetch_samples(gz_runner* r);
 /* clear_unique_states (supervisor_impl.cpp:138-144) at a generation roll (worker.py:160); safe while
  * the runner is running. */
 int gz_runner_clear_unique_states(gz_runner* r);
+/* Generation roll on a live runner (worker.py:138-160: Supervisor.update_nn + clear_unique_states):
+ * the launcher swaps in the new weights (blob: host float32, or device memory when device_blob,
+ * e.g. after an RCCL broadcast) between two launches, so every pool batch runs on exactly one
+ * network, then clears the duplicate filters if clear_unique_states.  Blocks until applied. */
+int gz_runner_update_network(gz_runner* r, const float* blob, size_t count, int device_blob,
+                             int clear_unique_states, double timeout_s);
+/* After a roll: pool_batches[i] = batches of pool i launched on the previous network;
+ * *launches_before = launches issued before the swap. */
+int gz_runner_roll_info(gz_runner* r, long* pool_batches, int npools, long* launches_before);
 const char* gz_runner_last_error(void);
 
 #ifdef __cplusplus

@@ -80,12 +80,14 @@ def _value_out(desc, z):
     return (_sigmoid(z) if getattr(desc, "value_sigmoid", False) else _softmax(z)).astype(np.float32)
 
 
-def forward(desc, weights, planes):
+def forward(desc, weights, planes, logits=False):
     """planes: float32 [N, C, H, W] (the poll() layout, cppinterface.py:114).
 
-    Returns [policy_0 [N,P_0], ..., policy_{R-1}, value [N,V]] float32 (model.py:294 order)."""
+    Returns [policy_0 [N,P_0], ..., policy_{R-1}, value [N,V]] float32 (model.py:294 order);
+    logits=True: the heads' pre-activation outputs (before the softmaxes / sigmoid), float64."""
     w = dict(weights)
     leaky = desc.leaky_relu
+    logits_out = logits
 
     def conv(x, name):
         y = _conv_same(x, w[name])
@@ -115,9 +117,9 @@ def forward(desc, weights, planes):
     outs = []
     for r in range(desc.role_count):
         h = _act(_bn(conv(x, "policy%d_conv" % r), w, "policy%d_bn" % r), leaky)
-        logits = _flatten(h, desc.flatten_nchw) @ w["policy%d_dense" % r].astype(np.float64)
-        logits = logits + w["policy%d_bias" % r]
-        outs.append(_softmax(logits).astype(np.float32))
+        logits_r = _flatten(h, desc.flatten_nchw) @ w["policy%d_dense" % r].astype(np.float64)
+        logits_r = logits_r + w["policy%d_bias" % r]
+        outs.append(logits_r if logits_out else _softmax(logits_r).astype(np.float32))
     v = conv(x, "value_conv")
     if getattr(desc, "value_bn", False):
         v = _bn(v, w, "value_bn")
@@ -127,7 +129,7 @@ def forward(desc, weights, planes):
         flat = np.concatenate([x.mean(axis=(1, 2)), flat], axis=1)
     hid = _act(flat @ w["value_hidden"].astype(np.float64) + w["value_hidden_bias"], leaky)
     val = hid @ w["value_dense"].astype(np.float64) + w["value_bias"]
-    outs.append(_value_out(desc, val))
+    outs.append(val if logits_out else _value_out(desc, val))
     return outs
 
 

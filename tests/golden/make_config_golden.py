@@ -3,6 +3,10 @@
 Run in the build container (the reference is not on the GPU box):
     PYTHONPATH=/root/reference/src python tests/golden/make_config_golden.py
 
+Regenerating executes the reference's module code (third-party, untrusted): run it only in an
+isolated sandbox such as this container.  The committed configs.json is the pin; no test imports
+the reference.
+
 It imports ggpzero.defs.confs / templates (py3-importable) and records every default the
 self-play hot path reads: the attrs defaults of PUCTEvaluatorConfig, PUCTPlayerConfig,
 SelfPlayConfig, NNModelConfig (confs.py:9-151), templates.base_puct_config() and

@@ -16,8 +16,6 @@ trimming and the two-boards-per-workgroup trunk above 256 rows, and the NN-free-
 Reference: src/cpp/supervisor.cpp:79-99,196-245, src/cpp/scheduler.cpp:132-205,
 src/cpp/selfplay.cpp:76-337.
 """
-import ctypes
-
 import attr
 import numpy as np
 import pytest
@@ -25,26 +23,10 @@ import pytest
 from galvanise_zero_amd.defs import templates
 from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS
 from galvanise_zero_amd.nn.weights import random_planes, random_weights, to_blob
+from gpu_helpers import Pinned
 from puct_harness import Setup, sample_key
 
 pytestmark = pytest.mark.gpu
-
-
-class Pinned(object):
-    """hipHostMalloc'd buffer (what the runner's pools use), viewed as a float32 numpy array."""
-
-    def __init__(self, n):
-        self.hip = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch / libgz_nn.so already loaded
-        self.hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
-        self.hip.hipHostFree.argtypes = [ctypes.c_void_p]
-        self.ptr = ctypes.c_void_p()
-        assert self.hip.hipHostMalloc(ctypes.byref(self.ptr), max(1, n) * 4, 0) == 0
-        self.a = np.ctypeslib.as_array(ctypes.cast(self.ptr, ctypes.POINTER(ctypes.c_float)), shape=(max(1, n),))[:n]
-
-    def free(self):
-        if self.ptr:
-            self.hip.hipHostFree(self.ptr)
-            self.ptr = None
 
 
 def _net(desc, seed, device):

@@ -1,0 +1,99 @@
+"""Generation roll on a live runner (the reference's worker.py:138-160: Supervisor.update_nn +
+clear_unique_states while self-play continues; cppinterface.py:146-147, supervisor_impl.cpp:138-144).
+
+gz_runner_update_network swaps the network between two launches (no pool batch runs on two
+networks) and clears the duplicate filters: a pool's own filter just before its engine thread
+delivers the pool's first batch on the new network, the shared filter at once.  With per-pool
+filters the run stays deterministic, so one pool replayed through the oracle -- network A's outputs
+for its batches before the roll, B's after, its filter cleared at the same batch -- must emit
+exactly the runner's samples.  With the shared filter (the reference's, nondeterministic across
+pools by design: quirk 8) the roll must complete, launches continue and the net must compute B.
+"""
+import numpy as np
+import pytest
+
+from galvanise_zero_amd.defs import templates
+from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS
+from galvanise_zero_amd.nn.weights import random_planes, random_weights, to_blob
+from puct_harness import Setup, sample_key
+
+pytestmark = pytest.mark.gpu
+
+
+def _suffix(s):
+    s = dict(s)
+    s["match_identifier"] = "_".join(s["match_identifier"].split("_")[-2:])
+    return s
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("per_pool", [True, False])
+def test_generation_roll_live_runner(per_pool, hip_device):
+    import attr
+    from galvanise_zero_amd._native import HipNet
+    from galvanise_zero_amd.runner import SelfPlayRunner
+    from oracle import puct_ref as P
+    desc = BASELINE_CONFIGS[2]["desc"]
+    setup = Setup("breakthrough")
+    t = setup.transformer
+    wa, wb = to_blob(random_weights(desc, 7921)), to_blob(random_weights(desc, 7922))
+    net = HipNet(desc, hip_device, "fp32")
+    net.set_weights(wa)
+    conf = templates.selfplay_config_template()
+    conf.evals_per_move = 8
+    conf.run_to_end_evals = 4
+    B, threads, ppt, seed, spin = 32, 2, 4, 20251017, 1000
+    r = SelfPlayRunner(net, setup.sm, t, conf, device=hip_device, num_threads=threads, pools_per_thread=ppt,
+                       batch_size=B, seed=seed, keep_samples=True, spin_yield_playouts=spin,
+                       min_launch_rows=128, max_launch_wait_us=2000, per_pool_unique_states=per_pool)
+    r.start()
+    r.wait_rows(threads * ppt * B * 300, timeout_s=300)
+    before = r.stats()
+    roll = r.update_network(wb, clear_unique_states=True)
+    r.wait_rows(before["rows"] + threads * ppt * B * 300, timeout_s=300)
+    r.stop()
+    st = r.stats()
+    samples = r.fetch_samples()
+    r.close()
+    print("roll", roll, "stats before", before, "after", st)
+    assert st["kernel_launches"] > roll["launches_before"] > 0
+    assert all(k > 0 for k in roll["pool_batches"]), roll
+    # the net now computes network B exactly (a fresh net with B's weights, bit for bit)
+    x = random_planes(desc, 64, 5)
+    fresh = HipNet(desc, hip_device, "fp32")
+    fresh.set_weights(wb)
+    for a, b in zip(net.forward(x), fresh.forward(x)):
+        assert np.array_equal(a, b)
+    if not per_pool:
+        assert st["samples"] > before["samples"]
+        return
+    # replay one pool through the oracle: A before the roll, B after, filter cleared at the roll
+    neta = HipNet(desc, hip_device, "fp32")
+    neta.set_weights(wa)
+    pool = 5
+    mine = [s for s in samples if int(s["match_identifier"].split("_")[1][1:]) == pool]
+    k = roll["pool_batches"][pool]
+    us = P.UniqueStates(setup.ref_planes.hash_mask(), 1000)
+    man = P.Manager(setup.ref_sm, setup.ref_planes, B, us, "t", seed, pool * B, list(t.policy_dist_count),
+                    t.num_rewards, setup.num_prev_states)
+    d = attr.asdict(conf)
+    for key in ("puct_config", "run_to_end_puct_config"):
+        d[key]["spin_yield_playouts"] = spin
+    man.start(d)
+    pred = (0, [np.zeros(0, np.float32)] * setup.sm.role_count, np.zeros(0, np.float32))
+    batch = 0
+    while len(man.samples) < len(mine) and batch < 5000:
+        if batch == k + 1:          # this poll delivers batch k, the pool's first on network B
+            us.lookup.clear()
+        buf = man.poll(*pred)
+        assert buf is not None
+        xb = buf.reshape(-1, t.num_channels, t.num_cols, t.num_rows)
+        outs = (neta if batch < k else net).forward(xb)
+        pred = (xb.shape[0], outs[:-1], outs[-1])
+        batch += 1
+    n = len(mine)
+    assert n >= 4 and len(man.samples) >= n, (n, len(man.samples))
+    got = [sample_key(setup, _suffix(s), True) for s in mine]
+    exp = [sample_key(setup, _suffix(s), False) for s in man.samples[:n]]
+    assert got == exp
+    print("pool %d: %d samples identical to the oracle across the roll at batch %d" % (pool, n, k))

@@ -84,7 +84,7 @@ def main():
             net.close()
             del os.environ["GZ_KERNEL_STAMPS"]
             print("variant %s N=%d trunk-kernel stamps (cycles per workgroup): input+conv0 %.0f, residual trunk %.0f, "
-                  "head 1x1 convs + features %.0f" % ((v, n) + tuple(st[1:4])), flush=True)
+                  "head 1x1 convs + features %.0f, dense heads %.0f" % ((v, n) + tuple(st[1:5])), flush=True)
             slope, icpt = np.polyfit(xs, ys, 1)
             conv_flops = 2 * base.hw * base.cnn_filter_size ** 2 * 9 * 2 * n
             print("variant %s N=%d: %.1f us per residual block (%.0f TFLOP/s in the trunk), %.1f us fixed"
