@@ -74,7 +74,8 @@ def parse():
     ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
                     help="trunk arithmetic: fp32 = split hi/lo bf16 operands, three MFMAs per product "
                          "(fp32-class accuracy, the reference runs fp32 TF; default where the kernel "
-                         "has it, F <= 128); bf16 = bf16 operands (default for the F = 256 configs)")
+                         "has it: F <= 128 on <= 8x8, F = 256 on <= 10x10); bf16 = bf16 operands "
+                         "(default for cfg 4, 13x13 x 256)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=60.0)
     ap.add_argument("--opening-seconds", type=float, default=30.0,
                     help="also report the GPU leg's rate over the first seconds of aging (the opening phase the "
@@ -86,6 +87,9 @@ def parse():
     ap.add_argument("--max-launch-wait-us", type=int, default=3000, help="... or its oldest pool waited this long")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for CPU-side tests)")
     ap.add_argument("--device", type=int, default=-1, help="GPU of every rank (-1: LOCAL_RANK; tests share one GPU)")
+    ap.add_argument("--roll", action="store_true",
+                    help="a generation roll before the warmup: rank 0's second weight blob goes to every rank "
+                         "(RCCL broadcast) and replaces the live runner's network (gz_runner_update_network)")
     ap.add_argument("--spin-yield", type=int, default=1000,
                     help="yield a game's coroutine after this many NN-free playouts (0: reference behaviour)")
     return ap.parse_args()
@@ -266,7 +270,9 @@ def main():
     evals = args.evals or BASELINE_CONFIGS[args.config]["evals"]
     sm, transformer, desc = setup_game(args.config)
     if args.precision is None:
-        args.precision = "fp32" if desc.cnn_filter_size <= 128 else "bf16"
+        # bf16x3 split wherever it is compiled: F <= 128 on boards <= 64 positions, F = 256 on boards
+        # <= 112 positions (single image); hexLG13's 12 x 256 on 13 x 13 (cfg 4) runs bf16
+        args.precision = "fp32" if desc.cnn_filter_size <= 128 or desc.hw <= 112 else "bf16"
     net = HipNet(desc, device, args.precision)
     heads_fused = net.heads_fused()
 
@@ -319,6 +325,16 @@ def main():
             heartbeat(runner.stats())
     aged = runner.stats()
     age_s = time.perf_counter() - t_start
+    # ---- optional generation roll on the live runner (worker.py:138-160) ----------------------------
+    roll, roll_sum = None, 0.0
+    if args.roll:
+        blob2 = torch.empty(net.weight_count, dtype=torch.float32, device="cuda")
+        if rank == 0:
+            blob2.copy_(torch.from_numpy(to_blob(random_weights(desc, 7922))))
+        shard.broadcast_weights(blob2, src=0)
+        torch.cuda.synchronize()
+        roll = runner.update_network(device_ptr=blob2.data_ptr(), count=net.weight_count, clear_unique_states=True)
+        roll_sum = float(blob2.double().sum().item())
     # ---- warmup + timed steps --------------------------------------------------------------------
     rows_base = aged["rows"]
     runner.wait_rows(rows_base + args.warmup * args.step_rows, timeout_s=3600, progress=heartbeat)
@@ -345,11 +361,11 @@ def main():
          d["kernel_launches"], d["segments"], d["completed_game_evals"], d["trunk_ms"],
          d["large_launches"], d["large_rows"], d["large_trunk_ms"], d["engine_idle_ms"],
          d["no_samples"], d["resigns"], d["aborts"], d["dupes"], d["tree_playouts"],
-         aged["games_completed"], games_per_rank, blob_sum, d["large_rounds"], d["split_launches"]],
+         aged["games_completed"], games_per_rank, blob_sum, d["large_rounds"], d["split_launches"], roll_sum],
         elapsed, device="cuda")
     (rows, batches, games, games_s, samples, kms, launches, segments, game_evals, tms,
      l_launches, l_rows, l_tms, idle_ms, no_samples, resigns, aborts, dupes, tree_playouts,
-     aged_games, games_total, blob_sums, l_rounds, split_launches) = totals
+     aged_games, games_total, blob_sums, l_rounds, split_launches, roll_sums) = totals
 
     if rank == 0:
         # host budget: leaf evaluations one engine thread sustains (this window) against what the
@@ -464,6 +480,10 @@ def main():
                          "flop_per_leaf": flops, "aggregate_tflops": flops * rows / T / 1e12},
             "gpu_busy_frac": (kms / 1e3) / (T * world) if T > 0 else None,
             "split_launches": split_launches,
+            "generation_roll": {"launches_before_rank0": roll["launches_before"],
+                                "collective": "RCCL broadcast" if world > 1 and args.backend == "nccl" else args.backend,
+                                "identical_on_all_ranks": abs(roll_sums - world * roll_sum) <= 1e-6 * max(1.0, abs(world * roll_sum))}
+                               if roll else None,
             "host_budget": {"leaf_evals_per_s_per_engine_thread": per_thread,
                             "gpu_forward_capacity_leaf_evals_per_s": gpu_capacity,
                             "engine_threads_per_gpu": threads, "engine_threads_needed_per_gpu": threads_needed,

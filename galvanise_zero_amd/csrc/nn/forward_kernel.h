@@ -87,6 +87,13 @@ struct KParams {
     int H, W, wmagic;        // board rows / columns; wmagic = ceil(65536 / W) (Board::div)
     int value_sigmoid;       // legacy model files: independent sigmoid per value output
     int logits;              // diagnostics (gz_net_set_output_logits): write pre-softmax / pre-sigmoid outputs
+    // policy heads as an MFMA GEMM (single-image nets with large policies, policy_gemm_kernel):
+    // packed weights [jt][kt][hi | lo][64 lanes][8] bf16 per role, logits scratch [n][sum P_r]
+    int gemm_heads;
+    const __bf16* pdp[kMaxRoles];
+    int pkt;                 // k-tiles of 32 per role (2HW padded)
+    float* glog;             // logits scratch
+    int plog;                // sum of P_r (row stride of glog)
     int v2;                  // pre-activation blocks: stream s += conv2(act(BN(conv1(act(BN(s)))))) [* SE gate]
     int k0taps;              // initial conv taps: 9 (3x3) or 1 (1x1, v2)
     int init_act;            // activation after the initial conv (0: v2 files with a bare initial conv)
@@ -125,6 +132,9 @@ __host__ __device__ constexpr int ring_depth(int nst, int ks, int ct, int cap) {
     return 1;
 }
 
+__host__ __device__ constexpr int gcd_c(int a, int b) { return b == 0 ? a : gcd_c(b, a % b); }
+__host__ __device__ constexpr int lcm_c(int a, int b) { return a / gcd_c(a, b) * b; }
+
 // P = 1: bf16 operands.  P = 3: split precision ("fp32 accuracy"): every fp32 operand x is carried
 // as x_hi = bf16(x), x_lo = bf16(x - x_hi) and each product as hi*hi + hi*lo + lo*hi (three MFMAs,
 // fp32 accumulation): ~16 significant bits per operand instead of 8.
@@ -142,13 +152,22 @@ struct Geo {
     // 256-byte row (WRAP), so hi + lo fit 512 bytes and two boards fit a workgroup's LDS (k-step
     // offsets then need an add + and per read: measured slower for the bf16 kernels, which keep
     // rows with room for the rotated chunks without wrap-around, profiles/r02h_kernel_variants_*)
-    static constexpr bool WRAP = CPR == 16 && P2 == 2;
-    static constexpr int HALF = WRAP ? 256 : ((CPR + 14) * 16 + 255) & ~255;   // one part's row
-    static constexpr int ROWS = P2 * HALF;           // LDS row stride: hi part, then lo part
-    // + one all-zero row (row kp.npos: every off-board 3x3 neighbour reads it) and one scratch row
-    // (row kp.npos + 1: the epilogues of a partial last position tile store their off-board lanes
-    // there instead of branching around the store)
-    static constexpr int ACT_BYTES = (NPOS + 2) * ROWS;
+    // (F = 256 split, single image: the same wrapped rotation inside 512-byte rows, so the hi + lo
+    // image of a 10 x 10 board fits the LDS)
+    //
+    // Padded rows (WRAP, the split kernels with >= 16 chunks per part): the rotation is replaced by
+    // a 32-byte pad per row -- row q, chunk c at byte q * ROWS + 16 c with ROWS = 2 * 16 CPR + 32,
+    // whose 16-byte bank group (34 q + c) mod 16 = (2 q + c) mod 16 is the rotated layout's --
+    // so a k-step's B reads differ by immediate offsets again (no add + and per read).  Off-board
+    // neighbours read a zero area (two rows) at the rotated chunk of their virtual position.
+    static constexpr bool WRAP = CPR >= 16 && P2 == 2;
+    static constexpr int HALF = WRAP ? CPR * 16 : ((CPR + 14) * 16 + 255) & ~255;   // one part's row
+    static constexpr int ROWS = WRAP ? P2 * HALF + 32 : P2 * HALF;   // LDS row stride: hi part, then lo part
+    static constexpr int ZROWS = WRAP ? 2 : 1;       // zero rows (padded rows: reads up to ROWS + 512)
+    // + the all-zero row(s) (from row kp.npos: every off-board 3x3 neighbour reads there) and one
+    // scratch row (row kp.npos + ZROWS: the epilogues of a partial last position tile store their
+    // off-board lanes there instead of branching around the store)
+    static constexpr int ACT_BYTES = (NPOS + ZROWS + 1) * ROWS;
     // k-steps per ring stage and the ring's VGPR budget: F = 256 (4 co tiles per wave, 16 weight
     // VGPRs per k-step) streams single k-steps through a 64-VGPR ring so the accumulators, the
     // residual and the B fragments still fit the 512 registers of a wave without spilling
@@ -156,7 +175,12 @@ struct Geo {
     static constexpr int NFR = CT * P2;              // weight fragments per k-step per lane
     static constexpr int ROWB = 64 * P2;             // bytes per output channel per k-step
     static constexpr int NST = 9 * KC / KS;          // ring stages per conv
-    static constexpr int R = ring_depth(NST, KS, NFR, CT >= 4 ? 64 : 96);
+    // ring depth; the two-board split kernels take exactly one tap's stages (R = KC / KS) so the
+    // looped conv's body is one tap (a deeper ring made the body three taps and spilled)
+    static constexpr int R = (P2 == 2 && NB == 2 && (KC / KS) >= 3 && NST % (KC / KS) == 0 &&
+                              (KC / KS) * KS * NFR * 4 <= 96)
+                                 ? KC / KS
+                                 : ring_depth(NST, KS, NFR, CT >= 4 ? 64 : 96);
     static constexpr int LPS = KS * NFR;             // weight loads per stage per lane
     // Single-image mode: when two ping-pong images (+ bias table) do not fit the 160 KB of LDS
     // (F = 256 on 10x10 / 13x13 boards), or the registers are nearly full anyway (large boards:
@@ -177,12 +201,23 @@ struct Geo {
     // (and the single-image ones) issue the ring with ordinary loads, which the compiler waits for.
     static constexpr bool TRACKED = SI || LIVE_VGPRS > 300 || (P2 == 2 && NB == 2);
     static_assert(F % 64 == 0, "filters must be a multiple of 64");
-    static_assert(P == 1 || (P == 3 && CT <= 2 && (NB == 1 || WRAP)), "split precision: F <= 128");
     static_assert(!SI || NB == 1, "single-image mode takes one board per workgroup");
     static_assert(!RG || SI, "the global residual is implemented for single-image kernels");
     static constexpr int RESID_BYTES = RG ? 4 * CT * TT * 64 * 16 : 0;   // per workgroup
     static_assert(KC % KS == 0, "a stage must not straddle a tap");
     static_assert(R >= 2, "no ring depth fits");
+    // Looped conv (two-image kernels): the 9-tap conv runs as NIT iterations of a body of U ring
+    // stages (a whole number of ring slots and of taps, an even number of k-steps so the B
+    // double buffer's parity is static) instead of fully unrolled: the unrolled conv pair of a
+    // residual block was ~100 KB of code, far beyond the instruction cache, so every block
+    // re-streamed its instructions (measured 21 cycles per MFMA with every memory access removed,
+    // against 16.5 for a register-only MFMA loop; profiles/r03bc_*).
+    static constexpr int SPT = KC / KS;                                  // ring stages per tap
+    static constexpr int U0 = lcm_c(R, SPT);
+    static constexpr int U = (U0 * KS) % 2 ? 2 * U0 : U0;                // stages per iteration
+    static constexpr int NIT = NST / U;
+    static constexpr int TPI = U * KS / KC;                              // taps per iteration
+    static constexpr bool LOOP = !SI && NST % U == 0 && NIT >= 2;
 };
 
 // chunk rotation of LDS row q (q may be a virtual, off-board position)
@@ -200,11 +235,14 @@ __host__ __device__ inline int bias_table_bytes(int F, int B) { return align16((
 // squeeze-excite scratch: per board the channel means [F] and the compressed units [kMaxSE]
 __host__ __device__ inline int se_scratch_bytes(int F, int NB) { return NB * (F + kMaxSE) * 4; }
 
-// ReLU / LeakyReLU(0.03) as max(v, alpha v) (alpha < 1): a multiply and a max, no compare / select
-// (a negative v gives -0.0 under ReLU instead of +0.0; every later use is unchanged by the sign)
 __device__ __forceinline__ float act_fn(float v, int leaky) {
-    return fmaxf(v, (leaky ? 0.03f : 0.f) * v);
+    return v > 0.f ? v : (leaky ? 0.03f * v : 0.f);
 }
+// The same activation as max(v, alpha v), alpha = 0 (ReLU) or 0.03 (LeakyReLU), alpha < 1: a
+// multiply and a max, no compare / select, for the two-image kernels' residual epilogues (a
+// negative v gives -0.0 under ReLU instead of +0.0; no later use depends on the sign).  (In the
+// single-image kernels this form raised register pressure: they keep act_fn.)
+__device__ __forceinline__ float act_mx(float v, float alpha) { return fmaxf(v, alpha * v); }
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
     __bf16 x = (__bf16)a, y = (__bf16)b;
@@ -213,13 +251,15 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 
 __device__ __forceinline__ float bf16_lo(float x) { return x - (float)(__bf16)x; }
 
-template <int F, int PTN, int P = 1>
+// SEL: off-board lanes of a partial last tile write the scratch row (a select, not a branch: the
+// two-image kernels); otherwise they branch around the store (single-image kernels, whose 40+ tile
+// epilogues keep fewer values live that way)
+template <int F, int PTN, int P = 1, bool SEL = true>
 __device__ __forceinline__ void store_act(char* X, int p, int co, f32x4 v, int npos) {
     using G = Geo<F, PTN, 1, P>;
-    {
-        // off-board lanes of a partial last tile write the scratch row (a select, not a branch)
-        const int q = p < npos ? p : npos + 1;
-        const int chunk = G::WRAP ? (((co >> 3) + swz(q)) & 15) : ((co >> 3) + swz(q));
+    if (SEL || p < npos) {
+        const int q = SEL && p >= npos ? npos + G::ZROWS : p;
+        const int chunk = G::WRAP ? (co >> 3) : ((co >> 3) + swz(q));
         char* a = X + q * G::ROWS + (chunk << 4) + (co & 7) * 2;
         uint2 u;
         u.x = pack2(v[0], v[1]);
@@ -327,13 +367,18 @@ __device__ __forceinline__ TapAddr tap_base(int tap, int pt, int lane, const Boa
     static_assert(PTN <= kMaxPTN, "board larger than the tap masks");
     const int qv = p + (dy * bd.W + dx);                 // the (virtual) neighbour position
     const bool ok = (bd.tapmask[pt] >> tap) & 1;
-    const int rot = G::WRAP ? (((g + swz(qv)) & 15) << 4) : ((g + swz(qv)) << 4);
+    if constexpr (G::WRAP) {   // padded rows: chunk g of row qv, or the zero area at the rotated chunk
+        const int a_in = qv * G::ROWS + (g << 4);
+        const int a_zero = bd.npos * G::ROWS + (((g + swz(qv)) & 15) << 4);
+        const int m = -(int)ok;    // both computed and masked: no divergent branch per tap and tile
+        return TapAddr{(a_in & m) | (a_zero & ~m), 0};
+    }
+    const int rot = (g + swz(qv)) << 4;
     return TapAddr{(ok ? qv : bd.npos) * G::ROWS, rot};
 }
 template <int F, int PTN, int P = 1>
 __device__ __forceinline__ int tap_offset(const TapAddr& t, int kc) {
-    using G = Geo<F, PTN, 1, P>;
-    return G::WRAP ? t.row + ((t.rot + 64 * kc) & 255) : t.row + t.rot + 64 * kc;
+    return t.row + t.rot + 64 * kc;
 }
 
 // One 3x3 'same' conv over the NB LDS images at X (board b at X + b*ACT_BYTES):
@@ -445,6 +490,100 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN,
                                std::make_integer_sequence<int, G::NST>{});
 }
 
+// ---- looped conv: one iteration = U ring stages = TPI taps; tap0 = the iteration's first tap ----
+// B fragments are single-buffered per tile: tile t's fragments for the next k-step are read right
+// after tile t's last MFMA of this k-step (the other tiles' MFMAs, ~670 cycles, cover the LDS
+// latency), which saves the 64 VGPRs of a second buffer; the register allocator otherwise shuffled
+// loop-carried values between VGPRs and AGPRs every iteration.
+template <int F, int PTN, int NB, int P, int ST>
+__device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+                                             f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
+                                             bf16x8 (&b)[Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
+                                             const __bf16* wres, uint32_t woff, int gs_it, int gmax, int& lane,
+                                             const Board& bd, int tap0, bool last_it) {
+    using G = Geo<F, PTN, NB, P>;
+    constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, KC = G::KC, P2 = G::P2;
+    static_assert(G::U % R == 0, "ring slots must be static within an iteration");
+    ring_issue<F, PTN, NB, P, (ST + R - 1) % R>(ring, wres, woff, gs_it + ST + R - 1, gmax);
+    if constexpr (!G::TRACKED) {
+        ring_wait<(R - 1) * G::LPS>();
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+            for (int f = 0; f < G::NFR; ++f) ring_ready(ring.r[ST % R][k][f]);
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+        const int jn = ST * KS + k + 1;           // the next k-step within the iteration
+        const int tap = tap0 + jn / KC, kc = jn % KC;   // and its tap
+        if (kc == 0) launder(lane);
+        int nb_off[PT];
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) nb_off[pt] = tap_offset<F, PTN, P>(tap_base<F, PTN, P>(tap, pt, lane, bd), kc);
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+            for (int pt = 0; pt < PT; ++pt) {
+                const int t = bb * PT + pt;
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) {
+                    const bf16x8 w_hi = ring.r[ST % R][k][ct * P2];
+                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][0], acc[ct][t], 0, 0, 0);
+                    if constexpr (P2 == 2) {
+                        const bf16x8 w_lo = ring.r[ST % R][k][ct * P2 + 1];
+                        acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][1], acc[ct][t], 0, 0, 0);
+                        acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[t][0], acc[ct][t], 0, 0, 0);
+                    }
+                }
+                {   // tile t of the next k-step (unconditional: past the conv's last k-step the tap
+                    // index is 9, whose mask bit is clear, so the reads hit the zero area)
+                    const char* a = X + nb_off[pt] + bb * G::ACT_BYTES;
+#pragma unroll
+                    for (int h = 0; h < P2; ++h) b[t][h] = *(const bf16x8*)(a + h * G::HALF);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, CT * (P2 == 2 ? 3 : 1), 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, P2, 0);                       // DS read
+            }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int F, int PTN, int NB, int P, int... ST>
+__device__ __forceinline__ void conv_iter(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+                                          f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
+                                          bf16x8 (&b)[Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
+                                          const __bf16* wres, uint32_t woff, int gs_it, int gmax, int& lane,
+                                          const Board& bd, int tap0, bool last_it, std::integer_sequence<int, ST...>) {
+    (conv_stage_l<F, PTN, NB, P, ST>(X, ring, acc, b, wres, woff, gs_it, gmax, lane, bd, tap0, last_it), ...);
+}
+
+template <int F, int PTN, int NB, int P>
+__device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+                                               f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
+                                               const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane,
+                                               const Board& bd) {
+    using G = Geo<F, PTN, NB, P>;
+    constexpr int PT = G::PT, TT = G::TT;
+#pragma unroll
+    for (int ct = 0; ct < G::CT; ++ct)
+#pragma unroll
+        for (int t = 0; t < TT; ++t) acc[ct][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 b[TT][G::P2];
+    launder(lane);
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) {
+        const char* a = X + tap_offset<F, PTN, P>(tap_base<F, PTN, P>(0, pt, lane, bd), 0);
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+            for (int h = 0; h < G::P2; ++h) b[bb * PT + pt][h] = *(const bf16x8*)(a + bb * G::ACT_BYTES + h * G::HALF);
+    }
+#pragma clang loop unroll(disable)
+    for (int it = 0; it < G::NIT; ++it)
+        conv_iter<F, PTN, NB, P>(X, ring, acc, b, wres, woff, gs0 + it * G::U, gmax, lane, bd, it * G::TPI,
+                                 it == G::NIT - 1, std::make_integer_sequence<int, G::U>{});
+}
+
 // Per-board channel sums over the board's positions of the wave's accumulator tiles: lane group g
 // (lanes 16g .. 16g+15) ends with the sums of channels co_base + 16ct + 4g + r in every lane.  The
 // order (tiles ascending, then a butterfly over the 16 lanes) depends only on the board.
@@ -535,6 +674,8 @@ __device__ __forceinline__ f32x4 pre_act(f32x4 v, const float4& sc, const float4
 template <int F, int PTN, int NB, int WPE, int P, bool V2>
 __device__ __forceinline__ void trunk_body(const KParams& kp) {
     using G = Geo<F, PTN, NB, P>;
+    static_assert(P == 1 || (P == 3 && (NB == 1 || G::WRAP) && (G::CT <= 2 || G::SI)),
+                  "split precision: F <= 128 (F = 256: single image)");
     constexpr int P2 = G::P2;
     constexpr int PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, kThreads = 256;
     const int NPOS = kp.npos, H = kp.H, W = kp.W;     // the board (NPOS <= G::NPOS)
@@ -608,8 +749,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     f32x4* rg = RG ? kp.resid + ((size_t)(blockIdx.x * 4 + wave) * CT * TT) * 64 + lane : nullptr;
 
     for (int i = tid; i < 2 * kp.B * F; i += kThreads) btab[i] = kp.bres[i];
-    for (int i = tid; i < NB * G::ROWS / 4; i += kThreads) {
-        const int bb = i / (G::ROWS / 4), j = i % (G::ROWS / 4);
+    for (int i = tid; i < NB * G::ZROWS * G::ROWS / 4; i += kThreads) {
+        const int bb = i / (G::ZROWS * G::ROWS / 4), j = i % (G::ZROWS * G::ROWS / 4);
         ((uint32_t*)(X0 + bb * ACT + NPOS * G::ROWS))[j] = 0u;
     }
 
@@ -724,13 +865,13 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                 if constexpr (RG) rg[(ct * TT + bb * PT + pt) * 64] = v;
                 else resid[ct][bb * PT + pt] = v;
                 acc[ct][bb * PT + pt] = v;    // the heads read acc when there is no residual block
-                store_act<F, PTN, P>(X0 + bb * ACT, 16 * pt + li, co, preact ? pre_act(v, psc, psh, kp.leaky) : v, NPOS);
+                store_act<F, PTN, P, !G::SI>(X0 + bb * ACT, 16 * pt + li, co, preact ? pre_act(v, psc, psh, kp.leaky) : v, NPOS);
             }
         }
         __syncthreads();    // scratch is reused by the next board
     }
-    for (int i = tid; i < NB * G::ROWS / 4; i += kThreads) {
-        const int bb = i / (G::ROWS / 4), j = i % (G::ROWS / 4);
+    for (int i = tid; i < NB * G::ZROWS * G::ROWS / 4; i += kThreads) {
+        const int bb = i / (G::ZROWS * G::ROWS / 4), j = i % (G::ZROWS * G::ROWS / 4);
         ((uint32_t*)(X1 + bb * ACT + NPOS * G::ROWS))[j] = 0u;
     }
     __syncthreads();
@@ -776,7 +917,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                         if constexpr (RG) rgc[(ct * TT + t) * 64] = v;
                         else resid[ct][t] = v;
                         acc[ct][t] = v;
-                        if (more) store_act<F, PTN, P>(X0, 16 * t + li, co, pre_act(v, psc, psh, kp.leaky), NPOS);
+                        if (more) store_act<F, PTN, P, !G::SI>(X0, 16 * t + li, co, pre_act(v, psc, psh, kp.leaky), NPOS);
                     }
                 }
                 __syncthreads();
@@ -805,17 +946,19 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                         else resid[ct][t] = v;
                         acc[ct][t] = v;
                     }
-                    store_act<F, PTN, P>(X0, 16 * t + li, co, v, NPOS);
+                    store_act<F, PTN, P, !G::SI>(X0, 16 * t + li, co, v, NPOS);
                 }
             }
             __syncthreads();
         }
     } else
     for (int blk = 0; blk < kp.B; ++blk) {
+        const float alpha = kp.leaky ? 0.03f : 0.f;
         const float* b_a = btab + (2 * blk) * F;
         const float* b_b = b_a + F;
 
-        conv3x3<F, PTN, NB, P>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd);
+        if constexpr (G::LOOP) conv3x3_looped<F, PTN, NB, P>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd);
+        else conv3x3<F, PTN, NB, P>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -823,16 +966,17 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
                 f32x4 v = acc[ct][t];
-                v[0] = act_fn(v[0] + bias.x, kp.leaky);
-                v[1] = act_fn(v[1] + bias.y, kp.leaky);
-                v[2] = act_fn(v[2] + bias.z, kp.leaky);
-                v[3] = act_fn(v[3] + bias.w, kp.leaky);
-                store_act<F, PTN, P>(X1 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);
+                v[0] = act_mx(v[0] + bias.x, alpha);
+                v[1] = act_mx(v[1] + bias.y, alpha);
+                v[2] = act_mx(v[2] + bias.z, alpha);
+                v[3] = act_mx(v[3] + bias.w, alpha);
+                store_act<F, PTN, P, !G::SI>(X1 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);
             }
         }
         __syncthreads();
 
-        conv3x3<F, PTN, NB, P>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane, bd);
+        if constexpr (G::LOOP) conv3x3_looped<F, PTN, NB, P>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane, bd);
+        else conv3x3<F, PTN, NB, P>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane, bd);
         if constexpr (V2) {   // s += SE(conv2 + bias); image = act(BN_1 of the next block (s)), model.py:128-149
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
@@ -859,7 +1003,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                     v[0] += r[0]; v[1] += r[1]; v[2] += r[2]; v[3] += r[3];
                     resid[ct][t] = v;
                     acc[ct][t] = v;
-                    if (more) store_act<F, PTN, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, pre_act(v, psc, psh, kp.leaky), NPOS);
+                    if (more) store_act<F, PTN, P, !G::SI>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, pre_act(v, psc, psh, kp.leaky), NPOS);
                 }
             }
             __syncthreads();
@@ -873,13 +1017,13 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
             for (int t = 0; t < TT; ++t) {
                 f32x4 v = acc[ct][t];
                 const f32x4 r = resid[ct][t];
-                v[0] = act_fn(v[0] + bias.x + r[0], kp.leaky);
-                v[1] = act_fn(v[1] + bias.y + r[1], kp.leaky);
-                v[2] = act_fn(v[2] + bias.z + r[2], kp.leaky);
-                v[3] = act_fn(v[3] + bias.w + r[3], kp.leaky);
+                v[0] = act_mx(v[0] + bias.x + r[0], alpha);
+                v[1] = act_mx(v[1] + bias.y + r[1], alpha);
+                v[2] = act_mx(v[2] + bias.z + r[2], alpha);
+                v[3] = act_mx(v[3] + bias.w + r[3], alpha);
                 resid[ct][t] = v;
                 acc[ct][t] = v;
-                store_act<F, PTN, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);
+                store_act<F, PTN, P, !G::SI>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);
             }
         }
         __syncthreads();
@@ -1037,7 +1181,15 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
         const int P = kp.P[r], K = 2 * NPOS;
         const float* Wd = kp.pd[r];
         const float* fr = fk + (size_t)r * 2 * NPOS * BPW;
-        for (int j = tid; j < P; j += 256) {
+        int lof = 0;
+        for (int q = 0; q < r; ++q) lof += kp.P[q];
+        if (kp.gemm_heads) {   // logits computed by policy_gemm_kernel (bias included)
+            for (int i = tid; i < nb * P; i += 256) {
+                const int b = i / P, j = i - b * P;
+                lg[b * LMAX + j] = kp.glog[(size_t)(board0 + b) * kp.plog + lof + j];
+            }
+        }
+        for (int j = tid; j < P && !kp.gemm_heads; j += 256) {
             float a[BPW];
 #pragma unroll
             for (int b = 0; b < BPW; ++b) a[b] = 0.f;
@@ -1133,6 +1285,65 @@ __host__ __device__ inline int fused_heads_bytes(int npos, int R, int maxP, int 
 // Separate heads launch (single-image trunk kernels: kHeadBoards boards per workgroup of features
 // from the device scratch).
 #ifdef GZNN_DEFINE_HEADS_KERNEL   // defined in one translation unit (gz_nn.hip)
+// Policy Dense(2HW -> P_r) of every board of a launch as one GEMM on MFMA (single-image nets with a
+// large policy, e.g. amazons P = 3041, where heads_kernel's per-4-board fp32 loop re-read 2.4 MB
+// of weights per role per 4 boards): logits[n][j] = sum_k f[n][k] W[k][j] + b[j], in split
+// precision (hi*hi + hi*lo + lo*hi, fp32 accumulation) whatever the trunk's mode, so the heads stay
+// fp32-class.  Grid (board tiles of 64, j-chunks of 128, roles); wave w takes boards
+// [64 bx + 16 w, +16) x the WG's 8 j-tiles of 16.  A = packed W^T fragments (row j, 8 k per lane),
+// B = the boards' features (col = board, 8 k per lane), split to hi / lo on the fly.
+__global__ void __launch_bounds__(256) policy_gemm_kernel(const KParams kp) {
+    const int r = blockIdx.z, P = kp.P[r], K = 2 * kp.npos;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int jt0 = blockIdx.y * 8;
+    const int njt = (P + 15) / 16;
+    if (jt0 >= njt) return;
+    const int board = blockIdx.x * 64 + wave * 16 + (lane & 15);
+    const int kq = 8 * (lane >> 4);
+    const float* f = kp.feat + (size_t)(board < kp.n ? board : 0) * kp.FS + (size_t)r * K;
+    f32x4 acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16x8* wp = (const bf16x8*)kp.pdp[r];
+    for (int kt = 0; kt < kp.pkt; ++kt) {
+        // B: this lane's 8 features (k = 32 kt + kq ..), zero past K or past the launch
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = 32 * kt + kq + e;
+            x[e] = (board < kp.n && k < K) ? f[k] : 0.f;
+        }
+        bf16x8 bh, bl;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            bh[e] = (__bf16)x[e];
+            bl[e] = (__bf16)(x[e] - (float)bh[e]);
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int jt = jt0 + t;
+            if (jt < njt) {
+                const size_t o = ((size_t)jt * kp.pkt + kt) * 128 + lane;   // [jt][kt][part][lane]
+                const bf16x8 ah = wp[o], al = wp[o + 64];
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[t], 0, 0, 0);
+            }
+        }
+    }
+    if (board >= kp.n) return;
+    int lof = 0;
+    for (int q = 0; q < r; ++q) lof += kp.P[q];
+    float* out = kp.glog + (size_t)board * kp.plog + lof;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const int j0 = (jt0 + t) * 16 + 4 * (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (j0 + i < P) out[j0 + i] = acc[t][i] + kp.pb[r][j0 + i];
+    }
+}
+
 __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
     constexpr int BPW = kHeadBoards;
     extern __shared__ __attribute__((aligned(16))) float hs[];

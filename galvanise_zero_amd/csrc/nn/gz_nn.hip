@@ -64,6 +64,8 @@ struct gz_net {
     int io_cap = 0;
     float last_ms = 0.f;
     int heads_smem = 0;
+    bool gemm_heads = false;       // policy heads by policy_gemm_kernel (single-image nets, large P)
+    std::map<hipStream_t, std::pair<float*, int>> glog;   // its logits scratch per stream
     std::mutex feat_mu;            // head-feature scratch, one per stream (launches on one stream are ordered)
     std::map<hipStream_t, std::pair<float*, int>> feat;
     std::map<hipStream_t, std::pair<char*, size_t>> resid;   // global-residual scratch per stream
@@ -196,6 +198,12 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     net->small = trunk(kc);
     net->large = trunk(kl);
     net->heads_smem = heads_lds_bytes(npos, d.role_count, maxP, d.value_hidden_size, gap_features(d));
+    // Large policies on nets whose every launch runs the separate heads kernel: the policy Dense
+    // layers run as one MFMA GEMM per launch (policy_gemm_kernel) instead of heads_kernel's
+    // per-4-board fp32 loop (amazons P = 3041: 12 % of the forward).  Every launch of such a net
+    // takes this path, so results stay batch-invariant.
+    net->gemm_heads = !net->small.fused_heads && !net->large.fused_heads && maxP >= 512 &&
+                      getenv("GZ_NO_GEMM_HEADS") == nullptr;
     KParams& kp = net->kp;
     kp.C = d.input_channels;
     kp.K0 = net->K0;
@@ -214,6 +222,10 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     kp.FS = (2 * d.role_count + 1) * npos + kp.gapF;
     kp.maxP = maxP;
     kp.npos = npos;
+    kp.gemm_heads = net->gemm_heads ? 1 : 0;
+    kp.pkt = (2 * npos + 31) / 32;
+    kp.plog = 0;
+    for (int r = 0; r < d.role_count; ++r) kp.plog += d.policy_dist_count[r];
     kp.H = d.input_columns;
     kp.W = d.input_rows;
     kp.wmagic = (65536 + kp.W - 1) / kp.W;
@@ -256,6 +268,7 @@ extern "C" void gz_net_destroy(gz_net* net) {
     if (net->d_stamps) (void)hipFree(net->d_stamps);
     for (auto& f : net->feat) (void)hipFree(f.second.first);
     for (auto& f : net->resid) (void)hipFree(f.second.first);
+    for (auto& f : net->glog) (void)hipFree(f.second.first);
     if (net->ev0) (void)hipEventDestroy(net->ev0);
     if (net->ev1) (void)hipEventDestroy(net->ev1);
     if (net->stream) (void)hipStreamDestroy(net->stream);
@@ -454,6 +467,29 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     const size_t o_vhw = L.alloc((size_t)VK * d.value_hidden_size * 4), o_vhb = L.alloc(d.value_hidden_size * 4);
     const size_t o_pre = L.alloc(pre.size() * 4), o_sew1 = L.alloc(sew1.size() * 4), o_sew2 = L.alloc(sew2.size() * 4);
     const size_t o_vdw = L.alloc((size_t)d.value_hidden_size * d.num_values * 4), o_vdb = L.alloc(d.num_values * 4);
+    // policy_gemm_kernel's A fragments: W^T tiles [jt][kt][hi | lo][64 lanes][8 k] bf16, lane l holding
+    // row j = 16 jt + l % 16 and k = 32 kt + 8 (l / 16) + e (zero padded)
+    std::vector<std::vector<uint16_t>> pdp(R);
+    size_t o_pdp[GZ_MAX_ROLES] = {};
+    if (net->gemm_heads) {
+        const int K = 2 * HW, nkt = (K + 31) / 32;
+        for (int r = 0; r < R; ++r) {
+            const int P = d.policy_dist_count[r], njt = (P + 15) / 16;
+            pdp[r].assign((size_t)njt * nkt * 2 * 64 * 8, 0);
+            for (int jt = 0; jt < njt; ++jt)
+                for (int kt = 0; kt < nkt; ++kt)
+                    for (int l = 0; l < 64; ++l)
+                        for (int e = 0; e < 8; ++e) {
+                            const int j = 16 * jt + (l & 15), k = 32 * kt + 8 * (l >> 4) + e;
+                            if (j >= P || k >= K) continue;
+                            const float v = pdense[r][(size_t)k * P + j];
+                            const size_t o = ((((size_t)jt * nkt + kt) * 2) * 64 + l) * 8 + e;
+                            pdp[r][o] = f2bf(v);
+                            pdp[r][o + 64 * 8] = lo_of(v);
+                        }
+            o_pdp[r] = L.alloc(pdp[r].size() * 2);
+        }
+    }
 
     std::vector<char> img(L.off, 0);
     auto put = [&](size_t off, const void* src, size_t bytes) { std::memcpy(img.data() + off, src, bytes); };
@@ -476,6 +512,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     put(o_vhb, vhb, d.value_hidden_size * 4);
     put(o_vdw, vdw, (size_t)d.value_hidden_size * d.num_values * 4);
     put(o_vdb, vdb, d.num_values * 4);
+    if (net->gemm_heads)
+        for (int r = 0; r < R; ++r) put(o_pdp[r], pdp[r].data(), pdp[r].size() * 2);
 
     HIPCHK(hipSetDevice(net->device));
     char* m = nullptr;
@@ -508,6 +546,7 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     kp.pre = (const float*)(m + o_pre);
     kp.sew1 = (const float*)(m + o_sew1);
     kp.sew2 = (const float*)(m + o_sew2);
+    for (int r = 0; r < R; ++r) kp.pdp[r] = net->gemm_heads ? (const __bf16*)(m + o_pdp[r]) : nullptr;
     net->has_weights = true;
     wl.unlock();
     if (old) {   // launches already queued may still read the old image
@@ -561,6 +600,21 @@ static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* se
             f.second = cap;
         }
         kp.feat = f.first;
+        kp.glog = nullptr;
+        if (net->gemm_heads) {
+            auto& g = net->glog[stream];
+            if (g.second < n) {
+                if (g.first) {
+                    HIPCHK(hipDeviceSynchronize());
+                    HIPCHK(hipFree(g.first));
+                    g.first = nullptr;
+                }
+                const int cap = std::max(n, 8192);
+                HIPCHK(hipMalloc((void**)&g.first, (size_t)cap * kp.plog * sizeof(float)));
+                g.second = cap;
+            }
+            kp.glog = g.first;
+        }
     }
     const gz_net::Trunk& t = n >= net->large_min_rows ? net->large : net->small;
     kp.resid = nullptr;
@@ -585,6 +639,12 @@ static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* se
     void* args[] = {&kp};
     HIPCHK(hipLaunchKernel(t.fn, dim3((n + t.nb - 1) / t.nb), dim3(256), args, t.smem, stream));
     if (mid) HIPCHK(hipEventRecord(mid, stream));
+    if (net->gemm_heads) {
+        int maxjt = 0;
+        for (int r = 0; r < kp.R; ++r) maxjt = std::max(maxjt, (kp.P[r] + 15) / 16);
+        HIPCHK(hipLaunchKernel((const void*)&policy_gemm_kernel, dim3((n + 63) / 64, (maxjt + 7) / 8, kp.R), dim3(256),
+                               args, 0, stream));
+    }
     if (!t.fused_heads)
         HIPCHK(hipLaunchKernel((const void*)&heads_kernel, dim3((n + kHeadBoards - 1) / kHeadBoards), dim3(256), args,
                                net->heads_smem, stream));

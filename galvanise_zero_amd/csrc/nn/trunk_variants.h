@@ -38,13 +38,17 @@ KernelChoice kernel_for() {
 template <int F, int PTN, bool V2 = false>
 KernelChoice variants(int v, int precision) {
     if (precision == 3) {
+        // F = 256 split: one board per workgroup in a single image of hi + lo wrapped rows, where
+        // that image and the bias table fit the LDS (10 x 10; a 13 x 13 image needs 182 KB)
+        if constexpr (F == 256) {
+            if constexpr (Geo<F, PTN, 1, 3>::SI && Geo<F, PTN, 1, 3>::ACT_BYTES + 40 * 1024 <= 160 * 1024 &&
+                          !Geo<F, PTN, 1, 3>::RG)
+                if (v == 11) return kernel_for<F, PTN, 1, 1, 3, V2>();
+            return KernelChoice{};
+        }
         if constexpr (F <= 128 && PTN <= 4) {
             if constexpr (2 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024) {
                 if (v == 11) return kernel_for<F, PTN, 1, 1, 3, V2>();
-                // one board per workgroup, two workgroups per CU (two waves per SIMD: one
-                // workgroup's epilogues and barriers overlap the other's MFMAs)
-                if constexpr (PTN == 4 && 4 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024)
-                    if (v == 12) return kernel_for<F, PTN, 1, 2, 3, V2>();
                 // two boards per workgroup (F = 128: 256-byte wrapped rows, hi + lo in 512 bytes)
                 if constexpr (Geo<F, PTN, 1, 3>::WRAP && 4 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024)
                     if (v == 21) return kernel_for<F, PTN, 2, 1, 3, V2>();

@@ -1,7 +1,7 @@
 """bench.py's own paths on the GPU: the single-rank line carries the contract's keys, and
 `--gpus 2` starts two ranks itself (torch.distributed.run) that broadcast the weight blob, load it
-with gz_net_set_weights_device, run the native runner on disjoint global game ranges and report
-n_gpus = 2.  The two ranks share GPU 0 over gloo here (one GPU per box; RCCL needs one GPU per
+with gz_net_set_weights_device, run the native runner on disjoint global game ranges, roll the live
+runners to a second broadcast generation (--roll) and report n_gpus = 2.  The two ranks share GPU 0 over gloo here (one GPU per box; RCCL needs one GPU per
 rank); the driver's 8-GPU run uses RCCL.  Reference: distributed/worker.py:107-160, SURVEY 8e."""
 import json
 import os
@@ -37,9 +37,11 @@ def test_bench_single_rank_line(hip_device):
 
 
 def test_bench_two_ranks(hip_device):
-    out = _run(["--gpus", "2", "--backend", "gloo", "--device", "0"] + SMALL, timeout=400)
+    out = _run(["--gpus", "2", "--backend", "gloo", "--device", "0", "--roll"] + SMALL, timeout=400)
     assert out["n_gpus"] == 2
     assert out["config"]["weights_broadcast"]["identical_on_all_ranks"] is True
+    # the mid-run generation roll: broadcast to both ranks, applied by both live runners
+    assert out["generation_roll"]["identical_on_all_ranks"] is True
     rng = out["config"]["game_ranges"]
     assert rng["disjoint"] is True and len(rng["per_rank"]) == 2
     assert rng["per_rank"][0][1] - rng["per_rank"][0][0] == out["config"]["games_per_gpu"]

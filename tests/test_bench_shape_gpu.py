@@ -27,10 +27,14 @@ TOL_FP32_KL = 5e-7
 # max(1, max |oracle logit|) of each output is the criterion; the probabilities' absolute error
 # then scales with the logits' magnitude (|dp| <= 2 max |dz|).  3x the worst measured on MI355X
 # (profiles/r03e_bench_shape_tests.log).
+# cfg4 / cfg5 run bf16 operands: their logits (scale ~700 / ~11,000) carry ~1 % relative error,
+# enough to flip a saturated softmax's argmax on some rows (probability error up to 1: the reason an
+# fp32-class mode matters for them), so for bf16 the mean probability error and the logits bound.
 TOL_DEEP = {   # name: (probs max, probs mean, logits max relative)
     "cfg3": (1.5e-3, 5e-6, 1.5e-4),
-    "cfg4": (5e-2, 5e-3, 0.1),
-    "cfg5": (5e-2, 5e-3, 0.1),
+    "cfg4": (1.0, 1e-3, 4e-2),
+    "cfg5_bf16": (1.0, 3e-2, 3e-2),
+    "cfg5": (5e-2, 1e-5, 1.5e-4),       # bf16x3 split, F = 256 on 10 x 10 (MFMA policy GEMM heads)
 }
 
 
@@ -95,7 +99,7 @@ def test_headline_trunk_at_bench_shape(hip_device):
         r0 += k
 
 
-DEEP = {"cfg3": (3, "fp32", 256), "cfg4": (4, "bf16", 256), "cfg5": (5, "bf16", 256)}
+DEEP = {"cfg3": (3, "fp32", 256), "cfg4": (4, "bf16", 256), "cfg5": (5, "fp32", 256), "cfg5_bf16": (5, "bf16", 256)}
 
 
 @pytest.mark.timeout(900)

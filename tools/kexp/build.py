@@ -6,6 +6,7 @@ libgz_engine.so.  Timing on the GPU box: GZ_LIB_DIR=tools/kexp/lib_<name> python
   base         unpatched (same-box reference)
   nostore      the residual epilogues compute but do not write the next LDS image (epilogue ds_writes)
   l1weights    every weight-ring stage reads stage 0's fragments (weights from L1 instead of L2)
+  unroll       the fully unrolled conv of round 2 instead of the looped one
   nobarrier    no workgroup barrier after the residual epilogues (results wrong; barrier cost)
   noaddr       every tap reads the centre tap's B addresses (no per-tap address arithmetic)
   noreads      no B-fragment LDS reads after each conv's first k-step
@@ -40,7 +41,7 @@ def patch(name, text):  # noqa: C901
         nonlocal text
         assert text.count(old) >= count, (name, old)
         text = text.replace(old, new)
-    if name == "base":
+    if name in ("base", "pad"):
         pass
     elif name == "nostore":
         rep("        *(uint2*)a = u;\n", "        if (npos < 0) *(uint2*)a = u;\n")
@@ -57,6 +58,8 @@ def patch(name, text):  # noqa: C901
             "            }\n        }\n        __syncthreads();\n    }\n",
             "                store_act<F, PTN, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);\n"
             "            }\n        }\n    }\n")
+    elif name == "unroll":
+        rep("    static constexpr bool LOOP = !SI && NST % U == 0 && NIT >= 2;\n", "    static constexpr bool LOOP = false;\n")
     elif name == "noaddr":
         rep("    const int dy = tap / 3 - 1, dx = tap % 3 - 1;\n", "    const int dy = 0, dx = 0;\n")
         rep("    const bool ok = (bd.tapmask[pt] >> tap) & 1;\n", "    const bool ok = (bd.tapmask[pt] >> 4) & 1;\n")

@@ -28,10 +28,10 @@ def main():
     from galvanise_zero_amd.nn.weights import random_weights, to_blob
     from galvanise_zero_amd.runner import SelfPlayRunner
     sm, t, desc = bench.setup_game(args.config)
-    net = HipNet(desc, 0)
+    # the bench's network: bf16x3 split where compiled, the bench's weights
+    net = HipNet(desc, 0, "fp32" if desc.cnn_filter_size <= 128 or desc.hw <= 112 else "bf16")
     net.set_weights(to_blob(random_weights(desc, 7921)))
-    cpus = len(os.sched_getaffinity(0))
-    threads = args.threads or max(1, min(15, cpus - 1))
+    threads = args.threads or max(1, bench.cpu_share() - 1)   # as bench.py (cgroup quota aware)
     conf = bench.selfplay_conf("template", BASELINE_CONFIGS[args.config]["evals"])
     r = SelfPlayRunner(net, sm, t, conf, device=0, num_threads=threads, pools_per_thread=args.pools,
                        batch_size=args.batch, seed=20251015, spin_yield_playouts=args.spin_yield,
