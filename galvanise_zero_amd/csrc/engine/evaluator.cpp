@@ -1089,13 +1089,15 @@ int PuctEvaluator::treePlayout(PuctNode* current, Path& path) {
 // the result stands when it is a win and beats every unwatched bound with margin (unwatched
 // elements below the final best cannot change the loop's outcome).
 
-static bool spin_fast_enabled() {
-    static const bool v = [] {
+// GZ_SPIN_FAST=0: no spin fast path; =2: the fast path without spinRunRegs (tests compare all three)
+static int spin_fast_mode() {
+    static const int v = [] {
         const char* e = std::getenv("GZ_SPIN_FAST");
-        return !(e != nullptr && e[0] == '0');
+        return e == nullptr || e[0] == '\0' ? 1 : std::atoi(e);
     }();
     return v;
 }
+static bool spin_fast_enabled() { return spin_fast_mode() != 0; }
 
 static inline double spin_margin_up(double x) { return x + std::fabs(x) * 1e-6 + 1e-12; }
 static inline double spin_margin_down(double x) { return x - std::fabs(x) * 1e-6 - 1e-12; }
@@ -1114,7 +1116,25 @@ bool PuctEvaluator::spinBuild() {
     const uint32_t v0 = node->visits;
     PuctNodeChild* cs = node->children();
     const int n = node->num_children;
+    // the children's fields from their mirrors in the child array (node.h) while those are exact:
+    // one streamed array instead of one cold node per child
+    const bool M = mirror_ok;
+    struct ChildView {
+        uint32_t visits;
+        float score;
+        uint16_t inflight;
+        bool finalised, all_unselectable;
+    };
+    auto view = [M, lead](const PuctNodeChild* c) {
+        const PuctNode* cn = c->to_node;
+        if (M)
+            return ChildView{c->m_visits, c->m_score, c->m_inflight, (c->m_flags & kMirrorFinalised) != 0,
+                             (c->m_flags & kMirrorAllUnselectable) != 0};
+        return ChildView{cn->visits, cn->getCurrentScore(lead), cn->inflight_visits, cn->is_finalised,
+                         cn->num_children > 0 && cn->unselectable_count == cn->num_children};
+    };
     int nw = 0, reach = 0, nvis = 0;
+    bool regs_ok = true;
     float win_score = 0.f;
     uint32_t wv0 = 0, wv1 = 0;   // the two largest win visit counts
     uint32_t nonwin_max_visits = 0;
@@ -1124,28 +1144,30 @@ bool PuctEvaluator::spinBuild() {
         const PuctNode* cn = c->to_node;
         if (c->unselectable) return false;
         if (cn != nullptr) {
-            if (cn->visits > 0) {
+            const ChildView cv = view(c);
+            if (cv.visits > 0) {
                 if (nvis == SpinEpoch::kMaxVisited) return false;
                 spin.visited[nvis++] = (uint16_t)i;
             }
-            if (cn->inflight_visits != 0) return false;
-            if (cn->num_children > 0 && cn->unselectable_count == cn->num_children) return false;
-            if (cn->is_finalised) {
-                const float sc = cn->getCurrentScore(lead);
+            if (cv.inflight != 0) return false;
+            if (cv.all_unselectable) return false;
+            if (cv.finalised) {
+                const float sc = cv.score;
                 if (sc > 0.99) {
                     if (!cn->isTerminal() || nw == SpinEpoch::kMaxWins) return false;
                     if (nw > 0 && !(sc == win_score)) return false;
+                    regs_ok = regs_ok && cn->num_children == 0;
                     win_score = sc;
                     ++nw;
-                    if (cn->visits >= wv0) { wv1 = wv0; wv0 = cn->visits; }
-                    else if (cn->visits > wv1) wv1 = cn->visits;
+                    if (cv.visits >= wv0) { wv1 = wv0; wv0 = cv.visits; }
+                    else if (cv.visits > wv1) wv1 = cv.visits;
                     ++reach;
                     continue;
                 }
                 if (sc < 0.01) continue;   // bad_fallback candidate: never reached while a candidate exists
             }
             have_nonwin_visits = true;
-            nonwin_max_visits = std::max(nonwin_max_visits, cn->visits);
+            nonwin_max_visits = std::max(nonwin_max_visits, cv.visits);
         }
         // a non-win candidate: the latch threshold only gets further away as v grows (checked
         // whether or not the latch is active yet: it may become active inside the epoch)
@@ -1188,10 +1210,11 @@ bool PuctEvaluator::spinBuild() {
                 base = prior_bound;
                 expl = pc * c->policy_prob * sq / (c->traversals + 1 + 0.0);
             } else {
-                const float sc = cn->getCurrentScore(lead);
-                if (cn->is_finalised && (sc > 0.99 || sc < 0.01)) continue;   // wins / bad fallbacks
+                const ChildView cv = view(c);
+                const float sc = cv.score;
+                if (cv.finalised && (sc > 0.99 || sc < 0.01)) continue;   // wins / bad fallbacks
                 base = sc;
-                expl = cn->is_finalised ? 0.0 : pc * c->policy_prob * sq / (c->traversals + 1 + 0.0);
+                expl = cv.finalised ? 0.0 : pc * c->policy_prob * sq / (c->traversals + 1 + 0.0);
             }
             const double u = spin_margin_up(base + expl);
             if (u < floor_adj) {
@@ -1211,7 +1234,7 @@ bool PuctEvaluator::spinBuild() {
             S.reserve(n);
             for (int i = 0; i < n; ++i) {
                 const PuctNode* cn = cs[i].to_node;
-                S.key_s[i] = cn == nullptr ? -1 : cn->getCurrentScore(lead);
+                S.key_s[i] = cn == nullptr ? -1 : view(cs + i).score;
                 S.key_p[i] = cs[i].policy_prob_orig;
             }
             const uint16_t* order = S.sortedOrder(n);
@@ -1219,7 +1242,7 @@ bool PuctEvaluator::spinBuild() {
             for (int j = 0; j < n; ++j) {
                 const int i = order[j];
                 const PuctNode* cn = cs[i].to_node;
-                if (cn != nullptr && cn->is_finalised && cn->getCurrentScore(lead) > 0.99) {
+                if (cn != nullptr && view(cs + i).finalised && S.key_s[i] > 0.99) {
                     spin.cand[k] = (uint16_t)i;
                     spin.cand_kind[k++] = SpinEpoch::kWin;
                     ++kw;
@@ -1238,6 +1261,7 @@ bool PuctEvaluator::spinBuild() {
             spin.ncand = k;
             spin.nvisited = nvis;
             spin.watch_prior = watch_prior;
+            spin.regs_ok = regs_ok && !watch_prior && sm->roleCount() <= kMaxRoles;
             spin.win_score = win_score;
             spin.unwatched_bound = unwatched;
             spin.conv_false = conv_false;
@@ -1277,11 +1301,15 @@ int PuctEvaluator::spinRun(int limit, bool multi) {
         }
     }
     if (!multi || !spin.conv_false) limit = 1;
+    const bool verify = verify_fastpath();
+    if (spin.regs_ok && !verify && spin_fast_mode() == 1) {
+        const int r = spinRunRegs(limit);
+        if (r >= 0) return r;
+    }
     const int lead = node->lead_role_index;
     const int role_count = sm->roleCount();
     PuctNodeChild* cs = node->children();
     const float limit_latch_root = 0.66;
-    const bool verify = verify_fastpath();
     int done = 0;
     while (done < limit && node->visits < spin.v_end) {
         // a playout that cannot take the fast path ends the run; it is the ordinary path's, at once
@@ -1420,6 +1448,282 @@ int PuctEvaluator::spinRun(int limit, bool multi) {
         stats.num_tree_playouts++;
         total_tree_playouts++;
         ++done;
+    }
+    return done;
+}
+
+// spinRun's playouts with the run's state in registers (the common epoch: no watched unexpanded
+// child, every win a childless terminal node): the selection and backup of the loop above,
+// operation for operation and in the same order, without the per-playout loads of the win nodes,
+// mirror refreshes and child-entry round trips through memory.  The candidates' traversals and
+// policy, the wins' visits and mirrors and the root's visits / scores / puct constant are written
+// back once at the end of the run (nothing else reads them inside it); the root-latch discards are
+// summed (Rng::discard only accumulates).  Steady-state engine probe (tools/engine_bench.cpp, one
+// thread): ~4-5 % less time per leaf than the loop above, trajectories identical.
+namespace {
+struct SpinRegs {
+    static constexpr int kC = 16;
+    float P[kC];            // policy_prob
+    uint32_t T[kC];         // traversals
+    float BASE[kC];         // current score of the parent's lead role
+    uint32_t LV[kC];        // the child node's visits
+    bool WIN[kC], FIN[kC];
+    float lsc[kC][kMaxRoles];
+    float cur[kMaxRoles];   // the root's current scores
+    int nc, lead, role_count;
+    bool noise_check;
+    float pc_root, pc;
+    double ub;
+    uint32_t v, v_end;
+    uint64_t reach, discards = 0;
+    uint32_t touched = 0;   // candidates chosen in this run (bit k)
+    int done = 0;
+    bool failed = false;
+};
+
+// backup()'s policy decay of the chosen child at the root (evaluator.cpp:605-625)
+inline void decay_params(float cur_score, float* apply, float* minimum) {
+    if (cur_score > 0.3 && cur_score < 0.7) {
+        *apply = 0.995;
+        *minimum = 0.02f;
+    } else if (cur_score > 0.15 && cur_score < 0.85) {
+        *apply = 0.9975;
+        *minimum = 0.03f;
+    } else {
+        *apply = 0.9975;
+        *minimum = 0.10f;
+    }
+}
+
+// Every candidate a win with the same scores: NC candidates at compile time, so their state lives
+// in registers.  (Deep in a spin -- root visits in the millions -- the wins' exploration terms differ
+// by less than a float ulp of their scores and the choice is decided by the rounding of the
+// reference's float `best_score`; the choice branches stay: predicted, they keep consecutive
+// playouts overlapping, where selects measured ~1.7x slower by making the choice a data dependency.)
+template <int NC, int R>
+__attribute__((noinline)) void spin_wins(SpinRegs& x, int limit) {
+    float P[NC];
+    uint32_t T[NC], LV[NC];
+    for (int k = 0; k < NC; ++k) { P[k] = x.P[k]; T[k] = x.T[k]; LV[k] = x.LV[k]; }
+    const float win_base = x.BASE[0];
+    float sc[R], cur[R];
+    const int lead = x.lead;
+    for (int ii = 0; ii < R; ii++) { sc[ii] = x.lsc[0][ii]; cur[ii] = x.cur[ii]; }
+    // cur[lead] with the role unrolled (a runtime index would keep cur in memory)
+    auto lead_score = [lead](const float* c) {
+        float r = c[0];
+        for (int ii = 1; ii < R; ii++) r = lead == ii ? c[ii] : r;
+        return r;
+    };
+    const float limit_latch_root = 0.66;
+    const float pc_root = x.pc_root;
+    const bool noise_check = x.noise_check;
+    const double ub = x.ub;
+    const uint32_t v_end = x.v_end;
+    const uint64_t reach = x.reach;
+    uint32_t v = x.v, touched = 0;
+    float pc = x.pc;
+    uint64_t discards = 0;
+    int done = 0;
+    bool failed = false;
+    while (done < limit && v < v_end) {
+        if (noise_check && lead_score(cur) <= 0.95) {
+            failed = true;
+            break;
+        }
+        pc = puct_log(v);
+        pc += pc_root;
+        const double sqrt_node_visits = std::sqrt(v + 1);
+        const bool latch = v > 1000 && v < 40000000;
+        bool latched_win = false;
+        for (int k = 0; k < NC; ++k) latched_win |= T[k] > 16 && T[k] > v * limit_latch_root;
+        if (latch && latched_win) {
+            failed = true;
+            break;
+        }
+        double child_score = win_base;
+        child_score *= 1.0f + pc;
+        float best_score = -1;
+        int best = -1;
+        double best_exact = 0.0;
+        for (int k = 0; k < NC; ++k) {
+            const int traversals = T[k] + 1;
+            const double inflight_visits = 0;
+            const double exploration_score = pc * P[k] * sqrt_node_visits / (traversals + inflight_visits);
+            const double score = child_score + exploration_score;
+            if (score > best_score) {
+                best = k;
+                best_score = score;
+                best_exact = score;
+            }
+        }
+        if (best < 0 || !(ub < best_exact) || !(ub <= (double)(float)best_exact)) {
+            failed = true;
+            break;
+        }
+        discards += latch ? reach : 0;
+        touched |= 1u << best;
+        for (int ii = 0; ii < R; ii++) {
+            float visits = v;
+            if (visits > 100000) visits = 100000 + 0.1f * (visits - 100000);
+            cur[ii] = ((visits * cur[ii] + sc[ii]) / (visits + 1.0f));
+        }
+        v++;
+        // the chosen candidate's updates through unrolled per-candidate predicates (compile-time
+        // indices keep the arrays in registers; an update at index `best` would put them in memory)
+        float apply = 1.0f, minimum = 0.0f;
+        const bool dec = v > 23;
+        if (dec) decay_params(lead_score(cur), &apply, &minimum);
+        for (int k = 0; k < NC; ++k) {
+            const bool ch = k == best;
+            LV[k] += ch;
+            T[k] += ch;
+            const float p = P[k];
+            float pn = p * apply;
+            pn = std::max(minimum, pn);
+            P[k] = ch && dec && p > minimum ? pn : p;
+        }
+        ++done;
+    }
+    for (int k = 0; k < NC; ++k) { x.P[k] = P[k]; x.T[k] = T[k]; x.LV[k] = LV[k]; }
+    for (int ii = 0; ii < R; ii++) x.cur[ii] = cur[ii];
+    x.v = v;
+    x.pc = pc;
+    x.discards += discards;
+    x.touched |= touched;
+    x.done += done;
+    x.failed = failed;
+}
+
+// any candidate mix (wins and watched scored children)
+void spin_mixed(SpinRegs& x, int limit) {
+    const float limit_latch_root = 0.66;
+    const int nc = x.nc, lead = x.lead, role_count = x.role_count;
+    while (x.done < limit && x.v < x.v_end) {
+        if (x.noise_check && x.cur[lead] <= 0.95) {
+            x.failed = true;
+            break;
+        }
+        const uint32_t v = x.v;
+        float pc = puct_log(v);
+        pc += x.pc_root;
+        x.pc = pc;
+        const double sqrt_node_visits = std::sqrt(v + 1);
+        const bool latch = v > 1000 && v < 40000000;
+        float best_score = -1;
+        int best = -1;
+        double best_exact = 0.0;
+        bool latched_win = false;
+        for (int k = 0; k < nc; ++k) {
+            if (x.WIN[k] && latch && x.T[k] > 16 && x.T[k] > v * limit_latch_root) {
+                latched_win = true;
+                break;
+            }
+            const int traversals = x.T[k] + 1;
+            const double inflight_visits = 0;
+            double exploration_score = pc * x.P[k] * sqrt_node_visits / (traversals + inflight_visits);
+            double child_score = x.BASE[k];
+            if (x.WIN[k]) child_score *= 1.0f + pc;
+            else if (x.FIN[k]) exploration_score = 0.0;
+            const double score = child_score + exploration_score;
+            if (score > best_score) {
+                best = k;
+                best_score = score;
+                best_exact = score;
+            }
+        }
+        if (latched_win || best < 0 || !x.WIN[best] || !(x.ub < best_exact) || !(x.ub <= (double)(float)best_exact)) {
+            x.failed = true;
+            break;
+        }
+        if (latch) x.discards += x.reach;
+        x.touched |= 1u << best;
+        x.LV[best]++;
+        for (int ii = 0; ii < role_count; ii++) {
+            float visits = v;
+            if (visits > 100000) visits = 100000 + 0.1f * (visits - 100000);
+            x.cur[ii] = ((visits * x.cur[ii] + x.lsc[best][ii]) / (visits + 1.0f));
+        }
+        x.v = v + 1;
+        x.T[best]++;
+        if (x.v > 23) {
+            float apply, minimum;
+            decay_params(x.cur[lead], &apply, &minimum);
+            if (x.P[best] > minimum) {
+                x.P[best] *= apply;
+                x.P[best] = std::max(minimum, x.P[best]);
+            }
+        }
+        ++x.done;
+    }
+}
+}  // namespace
+
+// Returns -1 when a precondition fails at entry (spinRun's loop then runs), else the playouts run
+// (0: the next playout takes the ordinary path, with spinRun's fail / fail_next convention).
+int PuctEvaluator::spinRunRegs(int limit) {
+    PuctNode* node = root;
+    PuctNodeChild* cs = node->children();
+    const int nc = spin.ncand;
+    if (node->inflight_visits != 0 || nc > SpinRegs::kC) return -1;
+    SpinRegs x;
+    x.nc = nc;
+    x.lead = node->lead_role_index;
+    x.role_count = sm->roleCount();
+    bool all_win = true;
+    for (int k = 0; k < nc; ++k) {
+        const PuctNodeChild* c = cs + spin.cand[k];
+        const PuctNode* cn = c->to_node;
+        if (cn == nullptr || cn->inflight_visits != 0) return -1;
+        x.P[k] = c->policy_prob;
+        x.T[k] = c->traversals;
+        x.BASE[k] = cn->getCurrentScore(x.lead);
+        x.LV[k] = cn->visits;
+        x.WIN[k] = spin.cand_kind[k] == SpinEpoch::kWin;
+        x.FIN[k] = cn->is_finalised;
+        if (x.WIN[k] && cn->num_children != 0) return -1;
+        for (int ii = 0; ii < x.role_count; ii++) {
+            x.lsc[k][ii] = cn->getCurrentScore(ii);
+            all_win = all_win && x.lsc[k][ii] == x.lsc[0][ii];
+        }
+        all_win = all_win && x.WIN[k];
+    }
+    for (int ii = 0; ii < x.role_count; ii++) x.cur[ii] = node->getCurrentScore(ii);
+    x.noise_check = !node->dirichlet_noise_set && conf->dirichlet_noise_pct >= 0;
+    x.pc_root = conf->puct_constant_root;
+    x.pc = node->puct_constant;
+    x.ub = spin.unwatched_bound;
+    x.v = node->visits;
+    x.v_end = spin.v_end;
+    x.reach = (uint64_t)spin.reach;
+    if (all_win && x.role_count == 2 && nc == 2) spin_wins<2, 2>(x, limit);
+    else if (all_win && x.role_count == 2 && nc == 3) spin_wins<3, 2>(x, limit);
+    else if (all_win && x.role_count == 2 && nc == 4) spin_wins<4, 2>(x, limit);
+    else spin_mixed(x, limit);
+    const int done = x.done;
+    // write back (a selection that failed still ran setPuctConstant)
+    if (done > 0 || x.failed) node->puct_constant = x.pc;
+    for (int k = 0; k < nc; ++k) {
+        if (!(x.touched & (1u << k))) continue;
+        PuctNodeChild* c = cs + spin.cand[k];
+        c->policy_prob = x.P[k];
+        c->traversals = x.T[k];
+        c->to_node->visits = x.LV[k];
+        c->to_node->syncParent();
+    }
+    if (done > 0) {
+        node->visits = x.v;
+        for (int ii = 0; ii < x.role_count; ii++) node->setCurrentScore(ii, x.cur[ii]);
+        node->syncParent();
+        if (x.v % 100 == 0) node->normaliseX();   // only at v_end (spinBuild)
+        stats.playouts_finals += done;
+        stats.num_tree_playouts += done;
+        total_tree_playouts += done;
+        rng.discard(x.discards);
+    }
+    if (x.failed) {
+        if (done == 0) spin.valid = false;
+        else spin.fail_next = true;
     }
     return done;
 }

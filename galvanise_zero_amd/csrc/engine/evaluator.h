@@ -120,9 +120,11 @@ private:
         bool conv_false = false;     // converged() proved false for the epoch
         bool valid = false;
         bool fail_next = false;      // spinRun: the next playout fails the fast path (seen in the last run)
+        bool regs_ok = false;        // spinRunRegs applies: no watched prior, every win a childless leaf
     };
     bool spinBuild();
     int spinRun(int limit, bool multi);
+    int spinRunRegs(int limit);
     SpinEpoch spin;
     Path spin_path;
 

@@ -184,21 +184,24 @@ def test_spin_yield_matches_oracle(small, spin):
 
 
 def test_spin_fast_path_identical():
-    """The root spin fast path (evaluator.cpp spinPlayout: root -> finalised win playouts without the
-    full selection pass) changes nothing: breakthrough 8x8 self-play with it on, off, and on with
+    """The root spin fast path (evaluator.cpp spinRun / spinRunRegs: root -> finalised win playouts
+    without the full selection pass) changes nothing: breakthrough 8x8 self-play with it on, off,
+    on without the register-resident runs, and on with
     GZ_VERIFY_FASTPATH=1 (every spin playout re-selected by the ordinary path, abort on mismatch)
     gives identical samples; the run reaches the multi-win spin (tree playouts >> evaluations)."""
     import subprocess
     import sys
     script = os.path.join(os.path.dirname(__file__), "native", "spin_check.py")
     outs = []
-    for env in ({"GZ_SPIN_FAST": "0"}, {"GZ_SPIN_FAST": "1"}, {"GZ_SPIN_FAST": "1", "GZ_VERIFY_FASTPATH": "1"}):
+    # GZ_SPIN_FAST=2: the fast path without the register-resident runs (evaluator.cpp spinRunRegs)
+    for env in ({"GZ_SPIN_FAST": "0"}, {"GZ_SPIN_FAST": "1"}, {"GZ_SPIN_FAST": "2"},
+                {"GZ_SPIN_FAST": "1", "GZ_VERIFY_FASTPATH": "1"}):
         e = dict(os.environ, **env)
         r = subprocess.run([sys.executable, script, "breakthrough", "16", "3000", "100"], env=e,
                            capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
-    assert outs[0] == outs[1] == outs[2]
+    assert outs[0] == outs[1] == outs[2] == outs[3]
     assert outs[0]["samples"] > 50 and outs[0]["tree_playouts"] > 3 * outs[0]["evaluations"]
 
 

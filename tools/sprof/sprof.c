@@ -2,6 +2,8 @@
  * SIGPROF every SPROF_US microseconds of process CPU time (default 500); the handler stores the
  * interrupted instruction pointer.  At exit the samples and /proc/self/maps go to
  * $SPROF_OUT (default /tmp/sprof.out); tools/sprof/report.py symbolizes them (addr2line -f -i).
+ * SPROF_START_S=<s> drops the samples of the first seconds (wall time; the kernel delivers at most
+ * one SIGPROF per tick, so sample counts are a poor clock).
  * Build: gcc -O2 -shared -fPIC tools/sprof/sprof.c -o /tmp/sprof.so */
 #define _GNU_SOURCE
 #include <signal.h>
@@ -9,17 +11,26 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/time.h>
+#include <time.h>
 #include <ucontext.h>
 
 #define MAXS (1 << 24)
 static unsigned long *samples;
 static volatile long nsamples, nskip;
 static long skip;   /* SPROF_SKIP: ignore the first samples (e.g. the opening of a run) */
+static double start_after;   /* SPROF_START_S: ignore samples in the first seconds of wall time */
+static struct timespec t_init;
+static double since_init(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (t.tv_sec - t_init.tv_sec) + 1e-9 * (t.tv_nsec - t_init.tv_nsec);
+}
 
 static void handler(int sig, siginfo_t *si, void *ctx) {
     (void)sig; (void)si;
     ucontext_t *uc = (ucontext_t *)ctx;
     if (__atomic_fetch_add(&nskip, 1, __ATOMIC_RELAXED) < skip) return;
+    if (start_after > 0 && since_init() < start_after) return;
     long i = __atomic_fetch_add(&nsamples, 1, __ATOMIC_RELAXED);
     if (i < MAXS) samples[i] = (unsigned long)uc->uc_mcontext.gregs[REG_RIP];
 }
@@ -31,6 +42,9 @@ __attribute__((constructor)) static void sprof_init(void) {
     sa.sa_sigaction = handler;
     sa.sa_flags = SA_SIGINFO | SA_RESTART;
     sigaction(SIGPROF, &sa, NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t_init);
+    const char *st = getenv("SPROF_START_S");
+    start_after = st ? atof(st) : 0;
     const char *sk = getenv("SPROF_SKIP");
     skip = sk ? atol(sk) : 0;
     const char *us = getenv("SPROF_US");
