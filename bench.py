@@ -379,22 +379,17 @@ def main():
         rows_per_launch = rows / launches if launches else float("nan")
         # the trunk kernel runs as one of two variants by launch size; the roofline is reported for
         # the variant that took more trunk time, the other one alongside
-        # kernels are compiled per (padded filters, 16-position tiles): trunk_kernel<F, PT, NB, WPE, P>
-        fpad = 64 if desc.cnn_filter_size <= 64 else 128 if desc.cnn_filter_size <= 128 else 256
-        geo = (fpad, (desc.hw + 15) // 16)
+        # the trunk kernels of small / large launches, as rocprofv3 names them (gz_net_kernel_name)
         p = 3 if args.precision == "fp32" else 1
-        variants = {
-            "gznn::trunk_kernel<%d, %d, 2, 1, %d>" % (geo + (p,)): (l_launches, l_rows, l_tms),
-            "gznn::trunk_kernel<%d, %d, 1, 1, %d>" % (geo + (p,)): (launches - l_launches, rows - l_rows, tms - l_tms),
-        }
+        k_large, k_small = net.kernel_name(True), net.kernel_name(False)
+        variants = {k_large: (l_launches, l_rows, l_tms)}
         # the same over the whole run (aging included): what a rocprofv3 summary of this command
         # averages over
-        whole = {
-            "gznn::trunk_kernel<%d, %d, 2, 1, %d>" % (geo + (p,)): (s1["large_launches"], s1["large_rows"], s1["large_trunk_ms"]),
-            "gznn::trunk_kernel<%d, %d, 1, 1, %d>" % (geo + (p,)): (s1["kernel_launches"] - s1["large_launches"],
-                                                                   s1["rows"] - s1["large_rows"],
-                                                                   s1["trunk_ms"] - s1["large_trunk_ms"]),
-        }
+        whole = {k_large: (s1["large_launches"], s1["large_rows"], s1["large_trunk_ms"])}
+        if k_small != k_large:
+            variants[k_small] = (launches - l_launches, rows - l_rows, tms - l_tms)
+            whole[k_small] = (s1["kernel_launches"] - s1["large_launches"], s1["rows"] - s1["large_rows"],
+                              s1["trunk_ms"] - s1["large_trunk_ms"])
         # two-image trunk kernels run the dense heads themselves (no heads launch): their algorithmic
         # work per leaf is then the whole forward's
         kernel_flops = desc.flops_per_eval() if heads_fused else desc.flops_trunk()
@@ -414,7 +409,7 @@ def main():
         # algorithmic FLOP/s is a third of the dense bf16 peak
         peak = PEAK_BF16_TFLOPS / p
         for name, pv in per_variant.items():
-            nb = 2 if name.endswith(", 2, 1, %d>" % p) else 1
+            nb = 2 if name == k_large and k_large != k_small else 1
             wg = pv["rows_per_launch"] / nb
             cus = max(min(wg, NUM_CUS), 1e-9)
             rate = wg * wbytes / (max(pv["avg_kernel_ms"], 1e-9) / 1e3) / cus / 1e9

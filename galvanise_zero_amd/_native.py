@@ -103,6 +103,10 @@ def nn_lib():
         lib.gz_net_heads_fused.restype = ctypes.c_int
         lib.gz_net_heads_fused.argtypes = [ctypes.c_void_p]
         lib.gz_net_set_output_logits.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.gz_net_kernel_name.restype = ctypes.c_char_p
+        lib.gz_net_kernel_name.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.gz_net_large_min_rows.restype = ctypes.c_int
+        lib.gz_net_large_min_rows.argtypes = [ctypes.c_void_p]
         lib.gz_nn_last_error.restype = ctypes.c_char_p
         lib._gz_typed = True
     return lib
@@ -216,6 +220,13 @@ class HipNet(object):
 
     def flops_per_eval(self):
         return self.lib.gz_net_flops_per_eval(self.handle)
+
+    def kernel_name(self, large):
+        """The trunk kernel of small (below large_min_rows) / large launches, as rocprofv3 names it."""
+        return self.lib.gz_net_kernel_name(self.handle, int(bool(large))).decode()
+
+    def large_min_rows(self):
+        return self.lib.gz_net_large_min_rows(self.handle)
 
     def heads_fused(self):
         """True when the large trunk variant runs the dense heads itself (no heads_kernel launch)."""

@@ -109,7 +109,7 @@ __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
 
 // the dense policy / value heads (defined with heads_kernel below; the two-image trunk kernels call
 // it themselves)
-template <int BPW>
+template <int BPW, int NT = 256>
 __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, float* lg, int board0, int nb);
 
 // The board geometry at run time (kernels are compiled per filter count and position-tile count):
@@ -138,7 +138,9 @@ __host__ __device__ constexpr int lcm_c(int a, int b) { return a / gcd_c(a, b) *
 // P = 1: bf16 operands.  P = 3: split precision ("fp32 accuracy"): every fp32 operand x is carried
 // as x_hi = bf16(x), x_lo = bf16(x - x_hi) and each product as hi*hi + hi*lo + lo*hi (three MFMAs,
 // fp32 accumulation): ~16 significant bits per operand instead of 8.
-template <int F, int PTN, int NB = 1, int P = 1>
+// WG = wave groups per workgroup: 1 (4 waves for NB boards) or 2 (8 waves, 2 per SIMD: group g takes
+// board g of the workgroup with NB = 1; the register budget is then 256 per wave)
+template <int F, int PTN, int NB = 1, int P = 1, int WG = 1>
 struct Geo {
     static constexpr int P2 = P == 3 ? 2 : 1;        // bf16 parts per operand
     // the board (H x W, runtime: kp.H / kp.W) has at most NPOS = 16 * PTN positions
@@ -177,7 +179,7 @@ struct Geo {
     static constexpr int NST = 9 * KC / KS;          // ring stages per conv
     // ring depth; the two-board split kernels take exactly one tap's stages (R = KC / KS) so the
     // looped conv's body is one tap (a deeper ring made the body three taps and spilled)
-    static constexpr int R = (P2 == 2 && NB == 2 && (KC / KS) >= 3 && NST % (KC / KS) == 0 &&
+    static constexpr int R = (P2 == 2 && (NB == 2 || WG == 2) && (KC / KS) >= 3 && NST % (KC / KS) == 0 &&
                               (KC / KS) * KS * NFR * 4 <= 96)
                                  ? KC / KS
                                  : ring_depth(NST, KS, NFR, CT >= 4 ? 64 : 96);
@@ -199,9 +201,10 @@ struct Geo {
     // accumulators + residual) the register allocator moves values between VGPRs and AGPRs, and a
     // copy of an inline-asm load's destination could be taken before the data lands; such kernels
     // (and the single-image ones) issue the ring with ordinary loads, which the compiler waits for.
-    static constexpr bool TRACKED = SI || LIVE_VGPRS > 300 || (P2 == 2 && NB == 2);
+    static constexpr bool TRACKED = SI || LIVE_VGPRS > 300 || (P2 == 2 && (NB == 2 || WG == 2));
     static_assert(F % 64 == 0, "filters must be a multiple of 64");
     static_assert(!SI || NB == 1, "single-image mode takes one board per workgroup");
+    static_assert(WG == 1 || (NB == 1 && !SI), "wave groups: one board per group, two images");
     static_assert(!RG || SI, "the global residual is implemented for single-image kernels");
     static constexpr int RESID_BYTES = RG ? 4 * CT * TT * 64 * 16 : 0;   // per workgroup
     static_assert(KC % KS == 0, "a stage must not straddle a tap");
@@ -308,9 +311,9 @@ __device__ __forceinline__ void ring_ready(bf16x8& v) { asm volatile("" : "+v"(v
 
 // ---- trunk -------------------------------------------------------------------------------------
 
-template <int F, int PTN, int NB, int P>
+template <int F, int PTN, int NB, int P, int WG = 1>
 struct Ring {
-    using G = Geo<F, PTN, NB, P>;
+    using G = Geo<F, PTN, NB, P, WG>;
     bf16x8 r[G::R][G::KS][G::NFR];    // fragment f = ct * P2 + part
 };
 
@@ -326,22 +329,22 @@ template <int P2, int ROWB, int FR>
 struct FragOff {
     static constexpr int value = (FR / P2) * 16 * ROWB + (FR % P2) * 64;
 };
-template <int F, int PTN, int NB, int P, int SLOT, int... FRS>
-__device__ __forceinline__ void ring_issue_k(Ring<F, PTN, NB, P>& ring, int k, uint32_t woff, const char* sb,
+template <int F, int PTN, int NB, int P, int WG, int SLOT, int... FRS>
+__device__ __forceinline__ void ring_issue_k(Ring<F, PTN, NB, P, WG>& ring, int k, uint32_t woff, const char* sb,
                                              std::integer_sequence<int, FRS...>) {
-    using G = Geo<F, PTN, NB, P>;
+    using G = Geo<F, PTN, NB, P, WG>;
     if constexpr (G::TRACKED)
         ((ring.r[SLOT][k][FRS] = *(const bf16x8*)(sb + woff + FragOff<G::P2, G::ROWB, FRS>::value)), ...);
     else
         ((ring.r[SLOT][k][FRS] = gload_issue<FragOff<G::P2, G::ROWB, FRS>::value>(woff, sb)), ...);
 }
-template <int F, int PTN, int NB, int P, int SLOT>
-__device__ __forceinline__ void ring_issue(Ring<F, PTN, NB, P>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
-    using G = Geo<F, PTN, NB, P>;
+template <int F, int PTN, int NB, int P, int WG, int SLOT>
+__device__ __forceinline__ void ring_issue(Ring<F, PTN, NB, P, WG>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
+    using G = Geo<F, PTN, NB, P, WG>;
     const int s = gs < gmax ? gs : gmax;
 #pragma unroll
     for (int k = 0; k < G::KS; ++k)
-        ring_issue_k<F, PTN, NB, P, SLOT>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * G::ROWB,
+        ring_issue_k<F, PTN, NB, P, WG, SLOT>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * G::ROWB,
                                            std::make_integer_sequence<int, G::NFR>{});
 }
 
@@ -384,16 +387,16 @@ __device__ __forceinline__ int tap_offset(const TapAddr& t, int kc) {
 // One 3x3 'same' conv over the NB LDS images at X (board b at X + b*ACT_BYTES):
 // acc[ct][t] = W * X (fp32 accumulate), tile t = b*PT + pt.  gs0 = global stage index of this
 // conv's first stage; on entry stages gs0 .. gs0+R-2 are in flight in ring slots 0..R-2.
-template <int F, int PTN, int NB, int P, int ST>
-__device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+template <int F, int PTN, int NB, int P, int WG, int ST>
+__device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                            f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                            bf16x8 (&b)[2][Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
                                            const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane,
                                            const Board& bd) {
-    using G = Geo<F, PTN, NB, P>;
+    using G = Geo<F, PTN, NB, P, WG>;
     constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC, P2 = G::P2;
     // refill the slot stage ST-1 consumed with stage ST+R-1, then wait for stage ST
-    ring_issue<F, PTN, NB, P, (ST + R - 1) % R>(ring, wres, woff, gs0 + ST + R - 1, gmax);
+    ring_issue<F, PTN, NB, P, WG, (ST + R - 1) % R>(ring, wres, woff, gs0 + ST + R - 1, gmax);
     if constexpr (!G::TRACKED) {
         ring_wait<(R - 1) * G::LPS>();
 #pragma unroll
@@ -449,27 +452,27 @@ __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, P
     }
 }
 
-template <int F, int PTN, int NB, int P, int... S>
-__device__ __forceinline__ void ring_prime(Ring<F, PTN, NB, P>& ring, const __bf16* wres, uint32_t woff, int gmax,
+template <int F, int PTN, int NB, int P, int WG, int... S>
+__device__ __forceinline__ void ring_prime(Ring<F, PTN, NB, P, WG>& ring, const __bf16* wres, uint32_t woff, int gmax,
                                            std::integer_sequence<int, S...>) {
-    (ring_issue<F, PTN, NB, P, S>(ring, wres, woff, S, gmax), ...);
+    (ring_issue<F, PTN, NB, P, WG, S>(ring, wres, woff, S, gmax), ...);
 }
 
-template <int F, int PTN, int NB, int P, int... ST>
-__device__ __forceinline__ void conv_stages(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+template <int F, int PTN, int NB, int P, int WG, int... ST>
+__device__ __forceinline__ void conv_stages(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                             f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                             bf16x8 (&b)[2][Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
                                             const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane,
                                             const Board& bd, std::integer_sequence<int, ST...>) {
-    (conv_stage<F, PTN, NB, P, ST>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd), ...);
+    (conv_stage<F, PTN, NB, P, WG, ST>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd), ...);
 }
 
-template <int F, int PTN, int NB, int P>
-__device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+template <int F, int PTN, int NB, int P, int WG = 1>
+__device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                         f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                         const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane,
                                         const Board& bd) {
-    using G = Geo<F, PTN, NB, P>;
+    using G = Geo<F, PTN, NB, P, WG>;
     constexpr int PT = G::PT, TT = G::TT;
 #pragma unroll
     for (int ct = 0; ct < G::CT; ++ct)
@@ -486,7 +489,7 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN,
 #pragma unroll
             for (int h = 0; h < G::P2; ++h) b[0][bb * PT + pt][h] = *(const bf16x8*)(a + bb * G::ACT_BYTES + h * G::HALF);
     }
-    conv_stages<F, PTN, NB, P>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd,
+    conv_stages<F, PTN, NB, P, WG>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd,
                                std::make_integer_sequence<int, G::NST>{});
 }
 
@@ -495,16 +498,16 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN,
 // after tile t's last MFMA of this k-step (the other tiles' MFMAs, ~670 cycles, cover the LDS
 // latency), which saves the 64 VGPRs of a second buffer; the register allocator otherwise shuffled
 // loop-carried values between VGPRs and AGPRs every iteration.
-template <int F, int PTN, int NB, int P, int ST>
-__device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+template <int F, int PTN, int NB, int P, int WG, int ST>
+__device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                              f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                              bf16x8 (&b)[Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
                                              const __bf16* wres, uint32_t woff, int gs_it, int gmax, int& lane,
                                              const Board& bd, int tap0, bool last_it) {
-    using G = Geo<F, PTN, NB, P>;
+    using G = Geo<F, PTN, NB, P, WG>;
     constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, KC = G::KC, P2 = G::P2;
     static_assert(G::U % R == 0, "ring slots must be static within an iteration");
-    ring_issue<F, PTN, NB, P, (ST + R - 1) % R>(ring, wres, woff, gs_it + ST + R - 1, gmax);
+    ring_issue<F, PTN, NB, P, WG, (ST + R - 1) % R>(ring, wres, woff, gs_it + ST + R - 1, gmax);
     if constexpr (!G::TRACKED) {
         ring_wait<(R - 1) * G::LPS>();
 #pragma unroll
@@ -548,21 +551,21 @@ __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F,
     }
 }
 
-template <int F, int PTN, int NB, int P, int... ST>
-__device__ __forceinline__ void conv_iter(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+template <int F, int PTN, int NB, int P, int WG, int... ST>
+__device__ __forceinline__ void conv_iter(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                           f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                           bf16x8 (&b)[Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
                                           const __bf16* wres, uint32_t woff, int gs_it, int gmax, int& lane,
                                           const Board& bd, int tap0, bool last_it, std::integer_sequence<int, ST...>) {
-    (conv_stage_l<F, PTN, NB, P, ST>(X, ring, acc, b, wres, woff, gs_it, gmax, lane, bd, tap0, last_it), ...);
+    (conv_stage_l<F, PTN, NB, P, WG, ST>(X, ring, acc, b, wres, woff, gs_it, gmax, lane, bd, tap0, last_it), ...);
 }
 
-template <int F, int PTN, int NB, int P>
-__device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<F, PTN, NB, P>& ring,
+template <int F, int PTN, int NB, int P, int WG = 1>
+__device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                                f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                                const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane,
                                                const Board& bd) {
-    using G = Geo<F, PTN, NB, P>;
+    using G = Geo<F, PTN, NB, P, WG>;
     constexpr int PT = G::PT, TT = G::TT;
 #pragma unroll
     for (int ct = 0; ct < G::CT; ++ct)
@@ -580,7 +583,7 @@ __device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<
     }
 #pragma clang loop unroll(disable)
     for (int it = 0; it < G::NIT; ++it)
-        conv_iter<F, PTN, NB, P>(X, ring, acc, b, wres, woff, gs0 + it * G::U, gmax, lane, bd, it * G::TPI,
+        conv_iter<F, PTN, NB, P, WG>(X, ring, acc, b, wres, woff, gs0 + it * G::U, gmax, lane, bd, it * G::TPI,
                                  it == G::NIT - 1, std::make_integer_sequence<int, G::U>{});
 }
 
@@ -671,9 +674,9 @@ __device__ __forceinline__ f32x4 pre_act(f32x4 v, const float4& sc, const float4
 // The trunk of NB boards per workgroup of 4 waves (trunk_kernel / trunk_kernel_v2 below).  V2:
 // pre-activation blocks with optional squeeze-excite (a separate instantiation, so the v1 kernels'
 // register allocation is not burdened by the v2 epilogues).
-template <int F, int PTN, int NB, int WPE, int P, bool V2>
+template <int F, int PTN, int NB, int WPE, int P, bool V2, int WG = 1>
 __device__ __forceinline__ void trunk_body(const KParams& kp) {
-    using G = Geo<F, PTN, NB, P>;
+    using G = Geo<F, PTN, NB, P, WG>;
     static_assert(P == 1 || (P == 3 && (NB == 1 || G::WRAP) && (G::CT <= 2 || G::SI)),
                   "split precision: F <= 128 (F = 256: single image)");
     constexpr int P2 = G::P2;
@@ -699,15 +702,19 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
 
     constexpr bool SI = G::SI, RG = G::RG;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* X0 = smem;                           // [NB][ACT]
-    char* X1 = SI ? smem : smem + NB * ACT;    // [NB][ACT]
+    // wave group grp (WG = 2: threads 256 grp .. 256 grp + 255) takes boards NB grp .. of the
+    // workgroup; LDS: image set 0 [WG][NB][ACT], image set 1 [WG][NB][ACT], bias table
+    const int grp = WG == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+    char* X0 = smem + grp * NB * ACT;                                  // [NB][ACT]
+    char* X1 = SI ? smem : smem + WG * NB * ACT + grp * NB * ACT;      // [NB][ACT]
     char* SCR = X1;                  // scratch aliases X1 while X1 holds no live activations
+    char* SCR0 = SI ? smem : smem + WG * NB * ACT;   // group 0's scratch (the fused heads' shared features)
     float* btab = (float*)(smem + kp.btab_off);   // trunk conv biases [2B][F], after X1 / scratch
 
-    const int board0 = blockIdx.x * NB;
-    const int tid = threadIdx.x;
+    const int board0 = (blockIdx.x * WG + grp) * NB;
+    const int tid = threadIdx.x & (kThreads - 1);   // within the group
 #define GZ_STAMP(i) \
-    if (kp.stamps && tid == 0) kp.stamps[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime()
+    if (kp.stamps && threadIdx.x == 0) kp.stamps[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime()
     GZ_STAMP(0);
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -740,15 +747,15 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     // prime the weight ring: stages 0 .. R-2 of the trunk stream
     const uint32_t woff = (uint32_t)((co_base + li) * G::ROWB + 16 * g);   // lane's fragment bytes within a k-step
     const int gmax = 2 * kp.B * G::NST - 1;
-    Ring<F, PTN, NB, P> ring;
-    if (kp.B > 0) ring_prime<F, PTN, NB, P>(ring, kp.wres, woff, gmax, std::make_integer_sequence<int, R - 1>{});
+    Ring<F, PTN, NB, P, WG> ring;
+    if (kp.B > 0) ring_prime<F, PTN, NB, P, WG>(ring, kp.wres, woff, gmax, std::make_integer_sequence<int, R - 1>{});
 
     f32x4 acc[CT][TT];
     f32x4 resid[RG ? 1 : CT][RG ? 1 : TT];
     // global residual of this wave: tile (ct, t) at rg[(ct * TT + t) * 64]
     f32x4* rg = RG ? kp.resid + ((size_t)(blockIdx.x * 4 + wave) * CT * TT) * 64 + lane : nullptr;
 
-    for (int i = tid; i < 2 * kp.B * F; i += kThreads) btab[i] = kp.bres[i];
+    for (int i = threadIdx.x; i < 2 * kp.B * F; i += kThreads * WG) btab[i] = kp.bres[i];
     for (int i = tid; i < NB * G::ZROWS * G::ROWS / 4; i += kThreads) {
         const int bb = i / (G::ZROWS * G::ROWS / 4), j = i % (G::ZROWS * G::ROWS / 4);
         ((uint32_t*)(X0 + bb * ACT + NPOS * G::ROWS))[j] = 0u;
@@ -883,7 +890,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         for (int cv = 0; cv < 2 * kp.B; ++cv) {
             const bool second = cv & 1;
             const float* bt = btab + cv * F;
-            conv3x3<F, PTN, NB, P>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane, bd);
+            conv3x3<F, PTN, NB, P, WG>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane, bd);
             __syncthreads();    // every wave has finished reading the image it is about to overwrite
             // residual tile addresses are formed here, not hoisted out of the loop (44 x 64-bit)
             f32x4* rgc = rg;
@@ -957,8 +964,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         const float* b_a = btab + (2 * blk) * F;
         const float* b_b = b_a + F;
 
-        if constexpr (G::LOOP) conv3x3_looped<F, PTN, NB, P>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd);
-        else conv3x3<F, PTN, NB, P>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd);
+        if constexpr (G::LOOP) conv3x3_looped<F, PTN, NB, P, WG>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd);
+        else conv3x3<F, PTN, NB, P, WG>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -975,8 +982,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         }
         __syncthreads();
 
-        if constexpr (G::LOOP) conv3x3_looped<F, PTN, NB, P>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane, bd);
-        else conv3x3<F, PTN, NB, P>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane, bd);
+        if constexpr (G::LOOP) conv3x3_looped<F, PTN, NB, P, WG>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane, bd);
+        else conv3x3<F, PTN, NB, P, WG>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane, bd);
         if constexpr (V2) {   // s += SE(conv2 + bias); image = act(BN_1 of the next block (s)), model.py:128-149
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
@@ -1061,12 +1068,15 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     }
     // FUSE (two-image kernels): the features stay in LDS, fk = [FS][NB], and the dense heads run
     // here; single-image kernels write them to the device scratch for heads_kernel
+    // (WG = 2: each group's 1x1 partials in its own scratch, the features of the workgroup's boards
+    // in group 0's, after its partials)
     constexpr bool FUSE = !SI;
-    float* fk = (float*)(SCR + align16(4 * HC * NPOS * 4));
-    float* lg = fk + align16(kp.FS * NB * 4) / 4;
+    constexpr int NBW = NB * WG;     // boards per workgroup
+    float* fk = (float*)(SCR0 + align16(4 * HC * NPOS * 4));
+    float* lg = fk + align16(kp.FS * NBW * 4) / 4;
     // feature k of board bb
     auto feat_at = [&](int bb, int k) -> float& {
-        if constexpr (FUSE) return fk[k * NB + bb];
+        if constexpr (FUSE) return fk[k * NBW + grp * NB + bb];
         else return kp.feat[(size_t)(board0 + bb) * kp.FS + k];
     };
 #pragma unroll
@@ -1139,8 +1149,9 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     }
     GZ_STAMP(3);
     if constexpr (FUSE) {
-        const int nb = kp.n - board0 < NB ? kp.n - board0 : NB;
-        dense_heads<NB>(kp, fk, lg, board0, nb);
+        const int wb0 = blockIdx.x * NBW;
+        const int nb = kp.n - wb0 < NBW ? kp.n - wb0 : NBW;
+        dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);
     }
     GZ_STAMP(4);
 #undef GZ_STAMP
@@ -1152,6 +1163,15 @@ template <int F, int PTN, int NB, int WPE, int P>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 trunk_kernel(const KParams kp) {
     trunk_body<F, PTN, NB, WPE, P, false>(kp);
+}
+
+// Two wave groups of 4 (8 waves, two per SIMD, a board per group): while one wave waits on a
+// barrier, an LDS read or its epilogue, the other wave of its SIMD issues MFMAs.  Same LDS as the
+// two-board kernel; each group streams the weights itself (twice the L2 weight traffic).
+template <int F, int PTN, int P>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+trunk_kernel8(const KParams kp) {
+    trunk_body<F, PTN, 1, 2, P, false, 2>(kp);
 }
 
 template <int F, int PTN, int NB, int WPE, int P>
@@ -1169,7 +1189,7 @@ trunk_kernel_v2(const KParams kp) {
 // the same operations for every BPW, so outputs do not depend on how boards are grouped (fused into
 // the trunk kernel with BPW = its NB, or in heads_kernel with BPW = 4).  Every thread of the
 // workgroup (4 waves) must call it; boards board0 .. board0 + nb - 1 are written.
-template <int BPW>
+template <int BPW, int NT>
 __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, float* lg, int board0, int nb) {
     static_assert(BPW >= 1 && BPW <= 4, "one softmax wave per board");
     const int NPOS = kp.npos;
@@ -1184,12 +1204,12 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
         int lof = 0;
         for (int q = 0; q < r; ++q) lof += kp.P[q];
         if (kp.gemm_heads) {   // logits computed by policy_gemm_kernel (bias included)
-            for (int i = tid; i < nb * P; i += 256) {
+            for (int i = tid; i < nb * P; i += NT) {
                 const int b = i / P, j = i - b * P;
                 lg[b * LMAX + j] = kp.glog[(size_t)(board0 + b) * kp.plog + lof + j];
             }
         }
-        for (int j = tid; j < P && !kp.gemm_heads; j += 256) {
+        for (int j = tid; j < P && !kp.gemm_heads; j += NT) {
             float a[BPW];
 #pragma unroll
             for (int b = 0; b < BPW; ++b) a[b] = 0.f;
@@ -1230,7 +1250,7 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
     {
         const int VH = kp.VH, VK = kp.gapF + NPOS;
         const float* fv = fk + (size_t)2 * kp.R * NPOS * BPW;
-        for (int j = tid; j < VH; j += 256) {
+        for (int j = tid; j < VH; j += NT) {
             float a[BPW];
 #pragma unroll
             for (int b = 0; b < BPW; ++b) a[b] = 0.f;

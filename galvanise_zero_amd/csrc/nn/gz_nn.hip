@@ -48,6 +48,8 @@ struct gz_net {
         int se_off = 0;            // LDS offset of the squeeze-excite scratch
         bool fused_heads = false;  // the dense heads run inside the trunk kernel (no heads_kernel launch)
         int resid_bytes = 0;       // global residual scratch per workgroup
+        int threads = 256;         // workgroup size (512: two wave groups)
+        std::string name;          // kernel name (rocprofv3's)
     } small, large;                // launches below / from large_min_rows rows
     int large_min_rows = 1 << 30;
     int p2 = 1;                    // bf16 parts per operand: 1 (bf16) or 2 (split precision)
@@ -152,8 +154,22 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     const int pt = (npos_ + 15) / 16;
     if (d.input_rows > 32 || npos_ >= 1024) { fail("board too large"); return nullptr; }
     const bool v2 = d.resnet_v2 != 0;
-    const KernelChoice kc = select_kernel(fpad, pt, vs, precision, v2);
+    KernelChoice kc = select_kernel(fpad, pt, vs, precision, v2);
     KernelChoice kl = select_kernel(fpad, pt, vl, precision, v2);
+    // wave-group kernels: each group's staging / heads scratch must fit its own image
+    auto wg_fits = [&](const KernelChoice& c) {
+        if (c.threads == 256) return true;
+        const int np = d.input_columns * d.input_rows;
+        int mp = 0;
+        for (int r = 0; r < d.role_count; ++r) mp = std::max(mp, d.policy_dist_count[r]);
+        const int kk0 = initial_kernel(d);
+        const int k0p = ((kk0 * kk0 * d.input_channels + 31) / 32) * 32;
+        const int p2 = precision == GZ_PRECISION_SPLIT ? 2 : 1;
+        return trunk_scratch_bytes(np, d.input_channels, k0p, d.role_count, p2) <= c.act_bytes &&
+               fused_heads_bytes(np, d.role_count, mp, d.value_hidden_size, gap_features(d), c.nb) <= c.act_bytes;
+    };
+    if (kl.fn && !wg_fits(kl)) kl = KernelChoice{};
+    if (kc.fn && !wg_fits(kc)) kc = KernelChoice{};
     if (kc.fn && !kl.fn && vl != vs) {   // geometries with a single (one board per workgroup) variant
         kl = kc;
         min_large = 1 << 30;
@@ -183,6 +199,8 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         gz_net::Trunk t;
         t.fn = c.fn;
         t.nb = c.nb;
+        t.threads = c.threads;
+        t.name = c.name;
         t.fused_heads = !c.single_image;
         const int scr = t.fused_heads ? std::max(scr_in, fused_heads_bytes(npos, d.role_count, maxP, d.value_hidden_size,
                                                                            gap_features(d), c.nb))
@@ -637,7 +655,7 @@ static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* se
     kp.btab_off = t.btab_off;
     kp.se_off = t.se_off;
     void* args[] = {&kp};
-    HIPCHK(hipLaunchKernel(t.fn, dim3((n + t.nb - 1) / t.nb), dim3(256), args, t.smem, stream));
+    HIPCHK(hipLaunchKernel(t.fn, dim3((n + t.nb - 1) / t.nb), dim3(t.threads), args, t.smem, stream));
     if (mid) HIPCHK(hipEventRecord(mid, stream));
     if (net->gemm_heads) {
         int maxjt = 0;
@@ -749,6 +767,11 @@ extern "C" int gz_net_set_output_logits(gz_net* net, int on) {
 }
 
 extern "C" int gz_net_large_min_rows(const gz_net* net) { return net ? net->large_min_rows : 0; }
+
+extern "C" const char* gz_net_kernel_name(const gz_net* net, int large) {
+    if (!net) return "";
+    return (large ? net->large : net->small).name.c_str();
+}
 
 extern "C" int gz_net_wave_rows(const gz_net* net) {
     if (!net) return 0;

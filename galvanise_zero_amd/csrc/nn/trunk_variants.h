@@ -12,6 +12,8 @@
 
 #include "forward_kernel.h"
 
+#include <cstdio>
+
 namespace gznn {
 
 struct KernelChoice {
@@ -20,6 +22,8 @@ struct KernelChoice {
     int nb = 1;
     bool single_image = false;
     int resid_bytes = 0;           // global residual scratch per workgroup (0: registers)
+    int threads = 256;             // workgroup size (512: two wave groups, trunk_kernel8)
+    char name[64] = {0};           // the kernel as rocprofv3 names it
 };
 
 template <int F, int PTN, int NB, int WPE, int P = 1, bool V2 = false>
@@ -31,10 +35,24 @@ KernelChoice kernel_for() {
     k.nb = NB;
     k.single_image = Geo<F, PTN, NB, P>::SI;
     k.resid_bytes = Geo<F, PTN, NB, P>::RESID_BYTES;
+    std::snprintf(k.name, sizeof(k.name), "gznn::trunk_kernel%s<%d, %d, %d, %d, %d>", V2 ? "_v2" : "", F, PTN, NB, WPE, P);
     return k;
 }
 
-// precision 3: split (hi / lo) operands; otherwise bf16.  v = NB * 10 + WPE.
+// two wave groups, one board each (variant 22)
+template <int F, int PTN, int P>
+KernelChoice kernel8_for() {
+    KernelChoice k;
+    k.fn = (const void*)&trunk_kernel8<F, PTN, P>;
+    k.act_bytes = Geo<F, PTN, 1, P, 2>::ACT_BYTES;
+    k.nb = 2;
+    k.threads = 512;
+    std::snprintf(k.name, sizeof(k.name), "gznn::trunk_kernel8<%d, %d, %d>", F, PTN, P);
+    return k;
+}
+
+// precision 3: split (hi / lo) operands; otherwise bf16.  v = NB * 10 + WPE; 22 = two boards as two
+// groups of four waves (trunk_kernel8).
 template <int F, int PTN, bool V2 = false>
 KernelChoice variants(int v, int precision) {
     if (precision == 3) {
@@ -50,8 +68,11 @@ KernelChoice variants(int v, int precision) {
             if constexpr (2 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024) {
                 if (v == 11) return kernel_for<F, PTN, 1, 1, 3, V2>();
                 // two boards per workgroup (F = 128: 256-byte wrapped rows, hi + lo in 512 bytes)
-                if constexpr (Geo<F, PTN, 1, 3>::WRAP && 4 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024)
+                if constexpr (Geo<F, PTN, 1, 3>::WRAP && 4 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024) {
                     if (v == 21) return kernel_for<F, PTN, 2, 1, 3, V2>();
+                    if constexpr (!V2)
+                        if (v == 22) return kernel8_for<F, PTN, 3>();
+                }
             }
         }
         return KernelChoice{};

@@ -116,6 +116,10 @@ float gz_net_last_kernel_ms(const gz_net* net);
  * the one-board variant (both compute every row identically). */
 int gz_net_large_min_rows(const gz_net* net);
 
+/* The trunk kernel of launches below (large = 0) / from (large = 1) gz_net_large_min_rows rows, as
+ * rocprofv3 names it (diagnostics: the bench reports its roofline per kernel). */
+const char* gz_net_kernel_name(const gz_net* net, int large);
+
 /* Rows one full wave of workgroups of the large variant covers (boards per workgroup x 256 CUs,
  * one trunk workgroup per CU): the native runner launches multiples of it beyond one wave. */
 int gz_net_wave_rows(const gz_net* net);

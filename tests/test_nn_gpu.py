@@ -246,9 +246,11 @@ def test_template_geometries(game, hint, hip_device):
             assert er[0] <= tol[0] and er[1] <= tol[1], (game, hint, precision, i, er)
 
 
-@pytest.mark.parametrize("variant", ["11", "21"])
+@pytest.mark.parametrize("variant", ["11", "21", "22"])
 def test_kernel_variants_identical_fp32(variant, hip_device, monkeypatch):
-    """The split-precision kernels (one or two boards per workgroup) compute every row identically."""
+    """The split-precision kernels (one or two boards per workgroup; 22: two boards as two groups of
+    four waves, trunk_kernel8) compute every row identically (33 rows: a dead board in the last
+    workgroup)."""
     from galvanise_zero_amd._native import HipNet
     desc = VARIANTS["cfg2"]
     x = random_planes(desc, 33, 4)
@@ -260,4 +262,22 @@ def test_kernel_variants_identical_fp32(variant, hip_device, monkeypatch):
     vnet = HipNet(desc, hip_device, "fp32")
     vnet.set_weights(w)
     for a, b in zip(base, vnet.forward(x)):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("n", [512, 1031])
+def test_wave_group_kernel_identical_at_bench_size(n, hip_device, monkeypatch):
+    """trunk_kernel8 (variant 22: 8 waves, one board per wave group) against the two-board kernel
+    (21) at launch sizes of the bench (one and three workgroup rounds): bit-identical."""
+    from galvanise_zero_amd._native import HipNet
+    desc = VARIANTS["cfg2"]
+    x = random_planes(desc, n, 6)
+    w = to_blob(random_weights(desc, 7921))
+    outs = []
+    for v in ("21", "22"):
+        monkeypatch.setenv("GZ_KERNEL_VARIANT", v)
+        net = HipNet(desc, hip_device, "fp32")
+        net.set_weights(w)
+        outs.append(net.forward(x))
+    for a, b in zip(*outs):
         assert np.array_equal(a, b)
