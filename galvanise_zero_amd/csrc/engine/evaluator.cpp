@@ -1302,10 +1302,87 @@ int PuctEvaluator::spinRun(int limit, bool multi) {
     }
     if (!multi || !spin.conv_false) limit = 1;
     const bool verify = verify_fastpath();
-    if (spin.regs_ok && !verify && spin_fast_mode() == 1) {
-        const int r = spinRunRegs(limit);
-        if (r >= 0) return r;
+    if (spin.regs_ok && spin_fast_mode() == 1) {
+        if (!verify) {
+            const int r = spinRunRegs(limit);
+            if (r >= 0) return r;
+        } else {
+            // verification: the register run, then the same run again from the same state through
+            // the loop below (whose every playout is re-selected by the ordinary path); the two end
+            // states must be identical
+            const SpinSnapshot before = spinSnapshot();
+            const int r = spinRunRegs(limit);
+            if (r >= 0) {
+                const SpinSnapshot regs = spinSnapshot();
+                spinRestore(before);
+                const int r2 = spinRunSlow(limit, true);
+                const SpinSnapshot slow = spinSnapshot();
+                if (r2 != r || !(regs == slow)) {
+                    std::fprintf(stderr, "gz spin register-run mismatch (visits %u, playouts %d vs %d)\n", node->visits,
+                                 r, r2);
+                    std::abort();
+                }
+                return r2;
+            }
+        }
     }
+    return spinRunSlow(limit, verify);
+}
+
+// Everything a spin run may change (the root's allocation -- header, child entries, scores --, the
+// candidates' node allocations, the epoch, the RNG and the counters), for GZ_VERIFY_FASTPATH.
+PuctEvaluator::SpinSnapshot PuctEvaluator::spinSnapshot() const {
+    SpinSnapshot s;
+    auto add = [&s](const PuctNode* n) {
+        const char* b = reinterpret_cast<const char*>(n);
+        s.bytes.insert(s.bytes.end(), b, b + n->allocated_size);
+    };
+    add(root);
+    // the child entries' debug scores are written by the verifying selection only (diagnostics)
+    for (int i = 0; i < root->num_children; ++i) {
+        PuctNodeChild* c = reinterpret_cast<PuctNodeChild*>(s.bytes.data() + sizeof(PuctNode)) + i;
+        c->debug_node_score = 0.f;
+        c->debug_puct_score = 0.f;
+    }
+    const PuctNodeChild* cs = root->children();
+    for (int k = 0; k < spin.ncand; ++k) add(cs[spin.cand[k]].to_node);
+    s.valid = spin.valid;
+    s.fail_next = spin.fail_next;
+    s.rng = rng;
+    s.playouts_finals = stats.playouts_finals;
+    s.num_tree_playouts = stats.num_tree_playouts;
+    s.total_tree_playouts = total_tree_playouts;
+    return s;
+}
+
+void PuctEvaluator::spinRestore(const SpinSnapshot& s) {
+    size_t o = 0;
+    auto put = [&s, &o](PuctNode* n) {
+        const size_t sz = n->allocated_size;
+        std::memcpy(reinterpret_cast<char*>(n), s.bytes.data() + o, sz);
+        o += sz;
+    };
+    PuctNodeChild* cs = root->children();
+    put(root);
+    for (int k = 0; k < spin.ncand; ++k) put(cs[spin.cand[k]].to_node);
+    spin.valid = s.valid;
+    spin.fail_next = s.fail_next;
+    rng = s.rng;
+    stats.playouts_finals = s.playouts_finals;
+    stats.num_tree_playouts = s.num_tree_playouts;
+    total_tree_playouts = s.total_tree_playouts;
+}
+
+bool PuctEvaluator::SpinSnapshot::operator==(const SpinSnapshot& o) const {
+    return bytes == o.bytes && valid == o.valid && fail_next == o.fail_next && rng == o.rng &&
+           playouts_finals == o.playouts_finals && num_tree_playouts == o.num_tree_playouts &&
+           total_tree_playouts == o.total_tree_playouts;
+}
+
+// spinRun's playouts one at a time through the node structures (the reference's operations in its
+// order); with `verify` every playout's choice is re-made by the ordinary selection.
+int PuctEvaluator::spinRunSlow(int limit, bool verify) {
+    PuctNode* node = root;
     const int lead = node->lead_role_index;
     const int role_count = sm->roleCount();
     PuctNodeChild* cs = node->children();

@@ -124,7 +124,18 @@ private:
     };
     bool spinBuild();
     int spinRun(int limit, bool multi);
+    int spinRunSlow(int limit, bool verify);
     int spinRunRegs(int limit);
+    struct SpinSnapshot {
+        std::vector<char> bytes;
+        bool valid = false, fail_next = false;
+        Rng rng;
+        int playouts_finals = 0, num_tree_playouts = 0;
+        long total_tree_playouts = 0;
+        bool operator==(const SpinSnapshot& o) const;
+    };
+    SpinSnapshot spinSnapshot() const;
+    void spinRestore(const SpinSnapshot& s);
     SpinEpoch spin;
     Path spin_path;
 

@@ -1,15 +1,17 @@
 // Forward of the residual policy/value CNN (v1, and v2 pre-activation with squeeze-excite and the
-// global-pooling value head) for gfx950 (MI355X): two launches per batch.
+// global-pooling value head) for gfx950 (MI355X).
 //
-// trunk_kernel: one workgroup (4 waves) evaluates NB boards through the whole trunk:
-//   planes (fp32 NCHW, HBM or pinned host) -> im2col in LDS -> initial conv -> B residual blocks
-//   -> the heads' 1x1 convs (+ the trunk's per-channel means for a pooling value head) -> per-board
-//   head features (fp32) to a device scratch.
-//   Trunk activations never leave the CU: the bf16 copy that feeds the next conv lives in LDS
-//   (two ping-pong images per board), the fp32 residual stream lives in the MFMA accumulators.
-// heads_kernel: one workgroup takes BPW boards' features and applies the policy Dense + softmax
-//   and value MLP + softmax in fp32 with the dense weights read once per BPW boards; the results go
-//   straight to the callers' buffers (segments).
+// trunk_kernel: one workgroup (4 waves; trunk_kernel8: two groups of 4 waves, a board each) takes
+// NB boards through the whole network:
+//   planes (fp32 NCHW, HBM staging or pinned host) -> im2col in LDS -> initial conv -> B residual
+//   blocks -> the heads' 1x1 convs (+ the trunk's per-channel means for a pooling value head) ->
+//   the dense policy / value heads + softmax, written straight to the callers' buffers (segments).
+//   Trunk activations never leave the CU: the bf16 (hi + lo in split precision) copy that feeds the
+//   next conv lives in LDS (two ping-pong images per board), the fp32 residual stream lives in
+//   registers.
+// Single-image kernels (F = 256 on 10 x 10 / 13 x 13: one image overwritten in place) write the head
+// features to a device scratch instead; heads_kernel (and policy_gemm_kernel for large policies)
+// then applies the dense heads.
 //
 // Each 3x3 conv is an implicit GEMM  out[co][p] = sum_{tap,ci} W[co][tap,ci] * X[nbr(p,tap)][ci]
 // on v_mfma_f32_16x16x32_bf16, A = weights (rows co), B = activations (cols = positions).  Wave w

@@ -77,7 +77,8 @@ int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_t count);
 
 /* One contiguous run of boards of a segmented launch.  Pointers may be device memory or pinned host
  * memory (hipHostMalloc): the kernel gathers planes from, and scatters outputs to, each segment
- * directly, so game pools need no staging copies. */
+ * directly.  (The native runner DMAs each launch's planes to an HBM staging buffer on a copy stream
+ * first and passes that as the planes; outputs go straight to the pools' pinned buffers.) */
 #define GZ_MAX_SEGMENTS 32
 typedef struct gz_segment {
     int rows;
@@ -86,10 +87,13 @@ typedef struct gz_segment {
     float* values;                            /* [rows][num_values] */
 } gz_segment;
 
-/* Asynchronous forward of up to GZ_MAX_SEGMENTS segments on `stream`: one trunk launch (planes ->
- * head features) and one heads launch (features -> policies / values) for all segments. */
+/* Asynchronous forward of up to GZ_MAX_SEGMENTS segments on `stream`.  Nets whose trunk kernel
+ * holds two activation images (F <= 128, and F = 256 up to 8 x 8) run the whole forward -- trunk and
+ * dense heads -- in one launch (gz_net_heads_fused); single-image nets (F = 256 on 10 x 10 / 13 x 13)
+ * launch the trunk (planes -> head features), then the policy GEMM for large policies, then the
+ * heads kernel. */
 int gz_net_forward_segments(gz_net* net, void* stream, const gz_segment* segs, int nseg);
-/* Same, recording `trunk_done_event` (a hipEvent_t, may be NULL) between the two launches so the
+/* Same, recording `trunk_done_event` (a hipEvent_t, may be NULL) after the trunk launch so the
  * caller can time the trunk kernel alone. */
 int gz_net_forward_segments_ev(gz_net* net, void* stream, const gz_segment* segs, int nseg,
                                void* trunk_done_event);
