@@ -239,6 +239,11 @@ def pin_rank_cpus(local_rank, local_world):
 
 def main():
     args = parse()
+    if os.environ.get("GZ_SPROF_LIB"):
+        # diagnostics: a host sampling profiler (tools/sprof/sprof.c) loaded into this process (its
+        # constructor arms SIGPROF; the samples are written at exit)
+        import ctypes
+        ctypes.CDLL(os.environ["GZ_SPROF_LIB"])
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))

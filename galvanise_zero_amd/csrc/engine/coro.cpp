@@ -53,7 +53,8 @@ extern "C" void gz_ctx_trampoline();
 namespace gz {
 
 static thread_local Coro t_root;
-static thread_local Coro* t_current = nullptr;
+// read at every switch: initial-exec (an %fs-relative load, no __tls_get_addr call)
+static thread_local Coro* t_current __attribute__((tls_model("initial-exec"))) = nullptr;
 
 Coro* coro_current() {
     if (t_current == nullptr) t_current = &t_root;

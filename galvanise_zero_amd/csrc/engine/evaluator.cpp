@@ -4,6 +4,7 @@
 // contraction behaviour depends on its unknown k273 build flags and is unpinned).
 #include "evaluator.h"
 
+#include "tls.h"
 #include "transformer.h"
 
 #include <algorithm>
@@ -471,7 +472,8 @@ struct SelectScratch {
     // sortedChildrenSelect permutation cache, keyed by the sort's input keys only: std::sort's
     // permutation is a function of the sequence of comparison outcomes, hence of the keys
     std::vector<float> cached_s, cached_p;
-    std::vector<uint16_t> perm;
+    std::vector<uint16_t> perm, perm2;
+    std::vector<uint8_t> mark;
     int cached_n = -1;
     struct Key {
         float s, p;
@@ -483,6 +485,7 @@ struct SelectScratch {
         if ((int)base.size() >= n) return;
         base.resize(n); expl.resize(n); inflight.resize(n); scores.resize(n); trav.resize(n);
         kind.resize(n); bcs.resize(n); key_s.resize(n); key_p.resize(n); perm.resize(n); tmp.resize(n);
+        perm2.resize(n); mark.resize(n);
         cached_s.resize(n); cached_p.resize(n);
     }
 
@@ -502,7 +505,6 @@ struct SelectScratch {
         return perm.data();
     }
 };
-thread_local SelectScratch t_sel;
 
 // child kinds of the selection pass
 enum : uint8_t { kSkip = 0, kPrior = 1, kScored = 2, kWinReturn = 3, kBad = 4 };
@@ -642,7 +644,7 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
         const char* p1 = reinterpret_cast<const char*>(cs + n);
         for (const char* q = p0; q < p1; q += 64) __builtin_prefetch(q, 1, 3);
     }
-    SelectScratch& S = t_sel;
+    SelectScratch& S = tls_instance<SelectScratch>();
     S.reserve(n);
     const int lead = node->lead_role_index;
     const bool latch = node->visits > 1000 && node->visits < 40000000 && depth == 0;
@@ -1089,6 +1091,33 @@ int PuctEvaluator::treePlayout(PuctNode* current, Path& path) {
 // the result stands when it is a win and beats every unwatched bound with margin (unwatched
 // elements below the final best cannot change the loop's outcome).
 
+// GZ_SPIN_STATS=1: spin fast-path counters (process totals, printed at exit; diagnostics only)
+namespace {
+enum SpinStat {
+    kSdBuilds, kSdBuildOk, kSdFailRoot, kSdFailUnselectable, kSdFailVisited, kSdFailInflight, kSdFailWinNode,
+    kSdFailWinScore, kSdFailLatch, kSdFailFewWins, kSdFailOrder, kSdFailWatched, kSdRegsPlayouts,
+    kSdSlowPlayouts, kSdOrdinaryPlayouts, kSdRetryWait, kSdCount
+};
+struct SpinStats {
+    const bool on = std::getenv("GZ_SPIN_STATS") != nullptr;
+    std::atomic<long> c[kSdCount] = {};
+    ~SpinStats() {
+        if (!on) return;
+        static const char* names[kSdCount] = {
+            "builds", "build_ok", "fail_root", "fail_unselectable", "fail_visited", "fail_inflight",
+            "fail_win_node", "fail_win_score", "fail_latch", "fail_few_wins", "fail_order", "fail_watched",
+            "regs_playouts", "slow_playouts", "ordinary_playouts", "retry_wait"};
+        std::fprintf(stderr, "gz spin stats:");
+        for (int i = 0; i < kSdCount; ++i) std::fprintf(stderr, " %s=%ld", names[i], c[i].load());
+        std::fprintf(stderr, "\n");
+    }
+};
+SpinStats g_spin_stats;
+inline void sd(SpinStat i, long n = 1) {
+    if (__builtin_expect(g_spin_stats.on, 0)) g_spin_stats.c[i].fetch_add(n, std::memory_order_relaxed);
+}
+}  // namespace
+
 // GZ_SPIN_FAST=0: no spin fast path; =2: the fast path without spinRunRegs (tests compare all three)
 static int spin_fast_mode() {
     static const int v = [] {
@@ -1103,37 +1132,30 @@ static inline double spin_margin_up(double x) { return x + std::fabs(x) * 1e-6 +
 static inline double spin_margin_down(double x) { return x - std::fabs(x) * 1e-6 - 1e-12; }
 
 bool PuctEvaluator::spinBuild() {
+    sd(kSdBuilds);
     spin.valid = false;
     PuctNode* node = root;
-    if (conf->backup_finalised || conf->think_time > 0) return false;
-    if (node->is_finalised || node->isTerminal() || node->num_children < 2 || node->visits <= 8) return false;
-    if (node->inflight_visits != 0) return false;
     const int lead = node->lead_role_index;
-    if (lead < 0) return false;
-    if (!node->dirichlet_noise_set && conf->dirichlet_noise_pct >= 0 && node->getCurrentScore(lead) <= 0.95)
+    if (conf->backup_finalised || conf->think_time > 0 || node->is_finalised || node->isTerminal() ||
+        node->num_children < 2 || node->visits <= 8 || node->inflight_visits != 0 || lead < 0 ||
+        (!node->dirichlet_noise_set && conf->dirichlet_noise_pct >= 0 && node->getCurrentScore(lead) <= 0.95)) {
+        sd(kSdFailRoot);
         return false;
+    }
 
     const uint32_t v0 = node->visits;
     PuctNodeChild* cs = node->children();
     const int n = node->num_children;
-    // the children's fields from their mirrors in the child array (node.h) while those are exact:
-    // one streamed array instead of one cold node per child
+    // One pass over the children gathers what the epoch needs into the thread's scratch (from their
+    // mirrors in the child array, node.h, while those are exact: one streamed array instead of one
+    // cold node per child): the sort keys, and the non-win candidates' selection terms.
     const bool M = mirror_ok;
-    struct ChildView {
-        uint32_t visits;
-        float score;
-        uint16_t inflight;
-        bool finalised, all_unselectable;
-    };
-    auto view = [M, lead](const PuctNodeChild* c) {
-        const PuctNode* cn = c->to_node;
-        if (M)
-            return ChildView{c->m_visits, c->m_score, c->m_inflight, (c->m_flags & kMirrorFinalised) != 0,
-                             (c->m_flags & kMirrorAllUnselectable) != 0};
-        return ChildView{cn->visits, cn->getCurrentScore(lead), cn->inflight_visits, cn->is_finalised,
-                         cn->num_children > 0 && cn->unselectable_count == cn->num_children};
-    };
-    int nw = 0, reach = 0, nvis = 0;
+    SelectScratch& S = tls_instance<SelectScratch>();
+    S.reserve(n);
+    enum : uint8_t { kUnexp = 0, kWinC = 1, kOther = 2, kSkipC = 3 };
+    uint8_t* kind = S.kind.data();   // (reused: the selection pass's kinds are dead here)
+    int nw = 0, reach = 0, nvis = 0, nother = 0;
+    uint16_t* other = S.perm2.data();   // non-win candidates
     bool regs_ok = true;
     float win_score = 0.f;
     uint32_t wv0 = 0, wv1 = 0;   // the two largest win visit counts
@@ -1142,39 +1164,66 @@ bool PuctEvaluator::spinBuild() {
     for (int i = 0; i < n; ++i) {
         const PuctNodeChild* c = cs + i;
         const PuctNode* cn = c->to_node;
-        if (c->unselectable) return false;
-        if (cn != nullptr) {
-            const ChildView cv = view(c);
-            if (cv.visits > 0) {
-                if (nvis == SpinEpoch::kMaxVisited) return false;
+        if (c->unselectable) return sd(kSdFailUnselectable), false;
+        S.key_p[i] = c->policy_prob_orig;
+        if (cn == nullptr) {
+            S.key_s[i] = -1;
+            kind[i] = kUnexp;
+        } else {
+            uint32_t visits;
+            float score;
+            uint16_t inflight;
+            bool finalised, all_unsel;
+            if (M) {
+                visits = c->m_visits;
+                score = c->m_score;
+                inflight = c->m_inflight;
+                finalised = (c->m_flags & kMirrorFinalised) != 0;
+                all_unsel = (c->m_flags & kMirrorAllUnselectable) != 0;
+            } else {
+                visits = cn->visits;
+                score = cn->getCurrentScore(lead);
+                inflight = cn->inflight_visits;
+                finalised = cn->is_finalised;
+                all_unsel = cn->num_children > 0 && cn->unselectable_count == cn->num_children;
+            }
+            S.key_s[i] = score;
+            S.base[i] = score;
+            if (visits > 0) {
+                if (nvis == SpinEpoch::kMaxVisited) return sd(kSdFailVisited), false;
                 spin.visited[nvis++] = (uint16_t)i;
             }
-            if (cv.inflight != 0) return false;
-            if (cv.all_unselectable) return false;
-            if (cv.finalised) {
-                const float sc = cv.score;
-                if (sc > 0.99) {
-                    if (!cn->isTerminal() || nw == SpinEpoch::kMaxWins) return false;
-                    if (nw > 0 && !(sc == win_score)) return false;
+            if (inflight != 0 || all_unsel) return sd(kSdFailInflight), false;
+            kind[i] = kOther;
+            S.bcs[i] = finalised;
+            if (finalised) {
+                if (score > 0.99) {
+                    if (!cn->isTerminal() || nw == SpinEpoch::kMaxWins) return sd(kSdFailWinNode), false;
+                    if (nw > 0 && !(score == win_score)) return sd(kSdFailWinScore), false;
                     regs_ok = regs_ok && cn->num_children == 0;
-                    win_score = sc;
+                    win_score = score;
                     ++nw;
-                    if (cv.visits >= wv0) { wv1 = wv0; wv0 = cv.visits; }
-                    else if (cv.visits > wv1) wv1 = cv.visits;
+                    if (visits >= wv0) { wv1 = wv0; wv0 = visits; }
+                    else if (visits > wv1) wv1 = visits;
                     ++reach;
+                    kind[i] = kWinC;
                     continue;
                 }
-                if (sc < 0.01) continue;   // bad_fallback candidate: never reached while a candidate exists
+                if (score < 0.01) {   // bad_fallback candidate: never reached while a candidate exists
+                    kind[i] = kSkipC;
+                    continue;
+                }
             }
             have_nonwin_visits = true;
-            nonwin_max_visits = std::max(nonwin_max_visits, cv.visits);
+            nonwin_max_visits = std::max(nonwin_max_visits, visits);
         }
         // a non-win candidate: the latch threshold only gets further away as v grows (checked
         // whether or not the latch is active yet: it may become active inside the epoch)
-        if (c->traversals > 16 && c->traversals > node->visits * 0.66f) return false;
+        if (c->traversals > 16 && c->traversals > node->visits * 0.66f) return sd(kSdFailLatch), false;
         ++reach;
+        other[nother++] = (uint16_t)i;
     }
-    if (nw < 2) return false;
+    if (nw < 2) return sd(kSdFailFewWins), false;
     // converged() (evaluator.cpp:1342-1362) compares the two most visited children: both wins with
     // equal scores -> false, and it stays false while only wins gain visits; otherwise playoutMain
     // evaluates it as usual
@@ -1193,6 +1242,7 @@ bool PuctEvaluator::spinBuild() {
     floor_win *= 1.0f + pc_at(v0);
     const double floor_adj = spin_margin_down(floor_win);
 
+    uint8_t* watched = S.mark.data();
     uint32_t v_end = (v0 / 100 + 1) * 100;   // normaliseX at the backup reaching a multiple of 100
     for (int attempt = 0; attempt < 4; ++attempt) {
         const uint32_t vl = v_end - 1;         // the epoch's last selection
@@ -1202,19 +1252,16 @@ bool PuctEvaluator::spinBuild() {
         int nwatch = 0;
         bool watch_prior = false;
         bool ok = true;
-        for (int i = 0; i < n && ok; ++i) {
+        for (int j = 0; j < nother && ok; ++j) {
+            const int i = other[j];
             const PuctNodeChild* c = cs + i;
-            const PuctNode* cn = c->to_node;
             double base, expl;
-            if (cn == nullptr) {
+            if (kind[i] == kUnexp) {
                 base = prior_bound;
                 expl = pc * c->policy_prob * sq / (c->traversals + 1 + 0.0);
             } else {
-                const ChildView cv = view(c);
-                const float sc = cv.score;
-                if (cv.finalised && (sc > 0.99 || sc < 0.01)) continue;   // wins / bad fallbacks
-                base = sc;
-                expl = cv.finalised ? 0.0 : pc * c->policy_prob * sq / (c->traversals + 1 + 0.0);
+                base = S.base[i];
+                expl = S.bcs[i] ? 0.0 : pc * c->policy_prob * sq / (c->traversals + 1 + 0.0);
             }
             const double u = spin_margin_up(base + expl);
             if (u < floor_adj) {
@@ -1222,46 +1269,37 @@ bool PuctEvaluator::spinBuild() {
             } else if (nwatch == SpinEpoch::kMaxWatched) {
                 ok = false;
             } else {
-                spin.watched_flag[nwatch++] = (uint16_t)i;   // temporarily: indices
-                watch_prior = watch_prior || cn == nullptr;
+                spin.watched_flag[nwatch++] = (uint16_t)i;
+                watch_prior = watch_prior || kind[i] == kUnexp;
             }
         }
         if (ok) {
             // wins and watched candidates in sortedChildrenSelect order (evaluator.cpp:242-263;
             // equal-score wins are equivalent under its comparator, so std::sort's permutation
             // decides)
-            SelectScratch& S = t_sel;
-            S.reserve(n);
-            for (int i = 0; i < n; ++i) {
-                const PuctNode* cn = cs[i].to_node;
-                S.key_s[i] = cn == nullptr ? -1 : view(cs + i).score;
-                S.key_p[i] = cs[i].policy_prob_orig;
-            }
+            std::memset(watched, 0, n);
+            for (int w = 0; w < nwatch; ++w) watched[spin.watched_flag[w]] = 1;
             const uint16_t* order = S.sortedOrder(n);
             int k = 0, kw = 0;
             for (int j = 0; j < n; ++j) {
                 const int i = order[j];
-                const PuctNode* cn = cs[i].to_node;
-                if (cn != nullptr && view(cs + i).finalised && S.key_s[i] > 0.99) {
+                if (kind[i] == kWinC) {
                     spin.cand[k] = (uint16_t)i;
                     spin.cand_kind[k++] = SpinEpoch::kWin;
                     ++kw;
-                    continue;
+                } else if (watched[i]) {
+                    spin.cand[k] = (uint16_t)i;
+                    spin.cand_kind[k++] = kind[i] == kUnexp ? SpinEpoch::kPrior : SpinEpoch::kScored;
                 }
-                for (int w = 0; w < nwatch; ++w)
-                    if (spin.watched_flag[w] == i) {
-                        spin.cand[k] = (uint16_t)i;
-                        spin.cand_kind[k++] = cn == nullptr ? SpinEpoch::kPrior : SpinEpoch::kScored;
-                        break;
-                    }
             }
             // (a comparator that is not a strict weak ordering -- the reference's, with negative
             // scores next to unexpanded children -- may drop or repeat elements: ordinary path)
-            if (kw != nw || k != nw + nwatch) return false;
+            if (kw != nw || k != nw + nwatch) return sd(kSdFailOrder), false;
             spin.ncand = k;
             spin.nvisited = nvis;
             spin.watch_prior = watch_prior;
             spin.regs_ok = regs_ok && !watch_prior && sm->roleCount() <= kMaxRoles;
+            sd(kSdBuildOk);
             spin.win_score = win_score;
             spin.unwatched_bound = unwatched;
             spin.conv_false = conv_false;
@@ -1275,6 +1313,7 @@ bool PuctEvaluator::spinBuild() {
         if (k == 0) break;
         v_end = v0 + k;
     }
+    sd(kSdFailWatched);
     return false;
 }
 
@@ -1293,7 +1332,7 @@ int PuctEvaluator::spinRun(int limit, bool multi) {
     }
     PuctNode* node = root;
     if (!spin.valid || spin.root != node || node->visits >= spin.v_end) {
-        if (spin.root == node && node->visits < spin.retry_at) return 0;
+        if (spin.root == node && node->visits < spin.retry_at) return sd(kSdRetryWait), 0;
         if (!spinBuild()) {
             spin.root = node;
             spin.retry_at = node->visits + 8;
@@ -1526,6 +1565,7 @@ int PuctEvaluator::spinRunSlow(int limit, bool verify) {
         total_tree_playouts++;
         ++done;
     }
+    sd(kSdSlowPlayouts, done);
     return done;
 }
 
@@ -1802,6 +1842,7 @@ int PuctEvaluator::spinRunRegs(int limit) {
         if (done == 0) spin.valid = false;
         else spin.fail_next = true;
     }
+    sd(kSdRegsPlayouts, done);
     return done;
 }
 
@@ -1873,6 +1914,7 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
             path.clear();
             depth = treePlayout(root, path);
             ran = 1;
+            sd(kSdOrdinaryPlayouts);
         }
         stats.playouts_max_depth = std::max(depth, stats.playouts_max_depth);
         stats.playouts_total_depth += depth * ran;

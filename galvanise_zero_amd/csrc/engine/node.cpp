@@ -1,5 +1,6 @@
 #include "node.h"
 
+#include "tls.h"
 #include "transformer.h"
 
 #include <algorithm>
@@ -39,12 +40,11 @@ struct NodeCache {
             }
     }
 };
-thread_local NodeCache t_node_cache;
 
 void* node_alloc(size_t bytes) {   // bytes: a multiple of 64
     const size_t c = bytes / 64;
     if (c < kNodeCacheClasses) {
-        NodeCache& nc = t_node_cache;
+        NodeCache& nc = tls_instance<NodeCache>();
         if (void* p = nc.head[c]) {
             nc.head[c] = *static_cast<void**>(p);
             nc.bytes -= bytes;
@@ -56,7 +56,7 @@ void* node_alloc(size_t bytes) {   // bytes: a multiple of 64
 
 void node_free(void* p, size_t bytes) {
     const size_t c = bytes / 64;
-    NodeCache& nc = t_node_cache;
+    NodeCache& nc = tls_instance<NodeCache>();
     if (c < kNodeCacheClasses && nc.bytes + bytes <= kNodeCacheBytes) {
         *static_cast<void**>(p) = nc.head[c];
         nc.head[c] = p;

@@ -19,6 +19,7 @@ static unsigned long *samples;
 static volatile long nsamples, nskip;
 static long skip;   /* SPROF_SKIP: ignore the first samples (e.g. the opening of a run) */
 static double start_after;   /* SPROF_START_S: ignore samples in the first seconds of wall time */
+static double stop_after;    /* SPROF_STOP_S: ... and after this many seconds (0: never) */
 static struct timespec t_init;
 static double since_init(void) {
     struct timespec t;
@@ -30,7 +31,10 @@ static void handler(int sig, siginfo_t *si, void *ctx) {
     (void)sig; (void)si;
     ucontext_t *uc = (ucontext_t *)ctx;
     if (__atomic_fetch_add(&nskip, 1, __ATOMIC_RELAXED) < skip) return;
-    if (start_after > 0 && since_init() < start_after) return;
+    if (start_after > 0 || stop_after > 0) {
+        const double t = since_init();
+        if (t < start_after || (stop_after > 0 && t > stop_after)) return;
+    }
     long i = __atomic_fetch_add(&nsamples, 1, __ATOMIC_RELAXED);
     if (i < MAXS) samples[i] = (unsigned long)uc->uc_mcontext.gregs[REG_RIP];
 }
@@ -45,6 +49,8 @@ __attribute__((constructor)) static void sprof_init(void) {
     clock_gettime(CLOCK_MONOTONIC, &t_init);
     const char *st = getenv("SPROF_START_S");
     start_after = st ? atof(st) : 0;
+    const char *sp = getenv("SPROF_STOP_S");
+    stop_after = sp ? atof(sp) : 0;
     const char *sk = getenv("SPROF_SKIP");
     skip = sk ? atol(sk) : 0;
     const char *us = getenv("SPROF_US");
