@@ -414,7 +414,7 @@ extern "C" int gz_player_root_children(gz_player* p, int* moves, uint32_t* trave
     const int lead = root->lead_role_index < 0 ? 0 : root->lead_role_index;
     for (int i = 0; i < n; ++i) {
         const PuctNodeChild* c = root->getNodeChild(0, i);
-        if (moves) moves[i] = c->move.get(lead);
+        if (moves) moves[i] = root->cold()[i].move.get(lead);
         if (traversals) traversals[i] = c->traversals;
         if (policy_probs) policy_probs[i] = c->policy_prob;
     }

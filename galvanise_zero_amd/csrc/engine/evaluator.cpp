@@ -181,7 +181,7 @@ PuctNode* PuctEvaluator::createNode(PuctNode* parent, const uint64_t* state) {
 // evaluator.cpp:216-239
 PuctNode* PuctEvaluator::expandChild(PuctNode* parent, PuctNodeChild* child) {
     sm->updateBases(parent->getBaseState());
-    sm->nextState(child->move, basestate_expand_node.data());
+    sm->nextState(parent->moveOf(child), basestate_expand_node.data());
 
     const int next_depth = parent->game_depth + 1;
     child->to_node = lookupNode(basestate_expand_node.data(), next_depth);
@@ -570,8 +570,8 @@ PuctNodeChild* PuctEvaluator::selectChildLiteral(PuctNode* node, int depth, floa
         }
 
         const float limit_latch_root = 0.66;
-        c->debug_node_score = child_score;
-        c->debug_puct_score = exploration_score;
+        node->coldOf(c).debug_node_score = child_score;
+        node->coldOf(c).debug_puct_score = exploration_score;
         const double score = child_score + exploration_score;
 
         if (node->visits > 1000 && node->visits < 40000000 && depth == 0 && rng.get() > 0.1) {
@@ -895,8 +895,9 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
                 const double discounted_visits = inflight_visits * (rng.get() + 0.5);
                 child_score = (child_score * trav) / (trav + discounted_visits);
             }
-            c->debug_node_score = child_score;
-            c->debug_puct_score = exploration_score;
+            PuctChildCold& cc = node->cold()[i];
+            cc.debug_node_score = child_score;
+            cc.debug_puct_score = exploration_score;
             const double score = child_score + exploration_score;
             if (latch && rng.get() > 0.1) {
                 if (trav > 16 && trav > node->visits * limit_latch_root) {
@@ -1379,7 +1380,8 @@ PuctEvaluator::SpinSnapshot PuctEvaluator::spinSnapshot() const {
     add(root);
     // the child entries' debug scores are written by the verifying selection only (diagnostics)
     for (int i = 0; i < root->num_children; ++i) {
-        PuctNodeChild* c = reinterpret_cast<PuctNodeChild*>(s.bytes.data() + sizeof(PuctNode)) + i;
+        PuctChildCold* c = reinterpret_cast<PuctChildCold*>(s.bytes.data() + sizeof(PuctNode) +
+                                                            sizeof(PuctNodeChild) * root->num_children) + i;
         c->debug_node_score = 0.f;
         c->debug_puct_score = 0.f;
     }
@@ -1968,7 +1970,7 @@ PuctNode* PuctEvaluator::fastApplyMove(const PuctNodeChild* next) {
 void PuctEvaluator::applyMove(const JointMove* move) {
     for (int ii = 0; ii < root->num_children; ii++) {
         PuctNodeChild* c = root->getNodeChild(0, ii);
-        if (c->move.equals(*move, sm->roleCount())) {
+        if (root->moveOf(c).equals(*move, sm->roleCount())) {
             fastApplyMove(c);
             break;
         }
@@ -2096,15 +2098,17 @@ Children PuctEvaluator::getProbabilities(PuctNode* node, float temperature, bool
     GZ_ASSERT(node->num_children > 0);
     const float node_visits = node->visits + 0.001 * node->num_children;
     float total_probability = 0.0f;
+    PuctChildCold* cold = node->cold();
     for (int ii = 0; ii < node->num_children; ii++) {
         PuctNodeChild* child = node->getNodeChild(0, ii);
+        float& next_prob = cold[ii].next_prob;
         const float child_visits = child->to_node ? child->traversals + 0.001f : 0.001f;
-        if (use_policy) child->next_prob = child->policy_prob + 0.001f;
-        else child->next_prob = child_visits / node_visits;
-        child->next_prob = (float)::pow((double)child->next_prob, (double)temperature);
-        total_probability += child->next_prob;
+        if (use_policy) next_prob = child->policy_prob + 0.001f;
+        else next_prob = child_visits / node_visits;
+        next_prob = (float)::pow((double)next_prob, (double)temperature);
+        total_probability += next_prob;
     }
-    for (int ii = 0; ii < node->num_children; ii++) node->getNodeChild(0, ii)->next_prob /= total_probability;
+    for (int ii = 0; ii < node->num_children; ii++) cold[ii].next_prob /= total_probability;
     return PuctNode::sortedChildren(node, true);
 }
 
@@ -2218,7 +2222,7 @@ const PuctNodeChild* PuctEvaluator::chooseTemperature(const PuctNode* node) {
     const float expected_probability = rng.get() * conf->random_scale;
     float seen_probability = 0;
     for (const PuctNodeChild* c : dist) {
-        seen_probability += c->next_prob;
+        seen_probability += root->coldOf(c).next_prob;
         if (seen_probability > expected_probability) return c;
     }
     return dist.back();
@@ -2241,13 +2245,13 @@ void PuctEvaluator::nodeDebug(int child_index, int max_variation_depth, PuctNode
     if (child->to_node == nullptr) return;
     info.lead_role_index = node->lead_role_index;
     info.score = child->to_node->getCurrentScore(node->lead_role_index);
-    info.move_index = child->move.get(node->lead_role_index);
+    info.move_index = node->moveOf(child).get(node->lead_role_index);
     const PuctNode* cur = child->to_node;
     for (int ii = 0; ii < max_variation_depth; ii++) {
         if (cur == nullptr || cur->num_children == 0 || cur->visits < 100) return;
         Children cc = PuctNode::sortedChildrenTraversals(cur, false);
         const PuctNodeChild* top = cc[0];
-        info.variation.emplace_back(cur->lead_role_index, top->move.get(cur->lead_role_index));
+        info.variation.emplace_back(cur->lead_role_index, cur->moveOf(top).get(cur->lead_role_index));
         cur = top->to_node;
     }
 }

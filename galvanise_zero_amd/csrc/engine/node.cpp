@@ -12,7 +12,8 @@ namespace gz {
 static_assert(sizeof(PuctNode) == 64, "node header must be one cache line");
 
 static size_t node_bytes(int num_children, int role_count, int num_words) {
-    size_t n = sizeof(PuctNode) + sizeof(PuctNodeChild) * num_children + sizeof(Score) * role_count;
+    size_t n = sizeof(PuctNode) + (sizeof(PuctNodeChild) + sizeof(PuctChildCold)) * num_children +
+               sizeof(Score) * role_count;
     n = (n + 7) & ~size_t(7);
     n += sizeof(uint64_t) * num_words;
     return (n + 63) & ~size_t(63);   // aligned_alloc: size is a multiple of the alignment
@@ -75,10 +76,10 @@ static int initialiseChildHelper(PuctNode* node, int role_index, int child_index
     for (int ii = 0; ii < n; ++ii) {
         joint_move->set(role_index, sm->legal(role_index, ii));
         if (final_role) {
+            PuctChildCold* cold = node->cold() + child_index;
             PuctNodeChild* child = node->getNodeChild(role_count, child_index++);
             child->to_node = nullptr;
             child->unselectable = false;
-            child->use_minimax = false;
             child->m_flags = 0;
             child->m_score = 0.0f;
             child->m_visits = 0;
@@ -86,10 +87,11 @@ static int initialiseChildHelper(PuctNode* node, int role_index, int child_index
             child->traversals = 0;
             child->policy_prob_orig = 1.0f;
             child->policy_prob = 1.0f;
-            child->next_prob = 0.0f;
-            child->debug_node_score = 0.0f;
-            child->debug_puct_score = 0.0f;
-            child->move = *joint_move;
+            cold->use_minimax = false;
+            cold->next_prob = 0.0f;
+            cold->debug_node_score = 0.0f;
+            cold->debug_puct_score = 0.0f;
+            cold->move = *joint_move;
         } else {
             child_index = initialiseChildHelper(node, role_index + 1, child_index, role_count, sm, joint_move);
         }
@@ -182,11 +184,11 @@ Children PuctNode::sortedChildren(const PuctNode* node, bool next_probability) {
     Children children;
     children.reserve(node->num_children);
     for (int ii = 0; ii < node->num_children; ii++) children.push_back(node->getNodeChild(0, ii));
-    auto f = [next_probability](const PuctNodeChild* a, const PuctNodeChild* b) {
+    auto f = [next_probability, node](const PuctNodeChild* a, const PuctNodeChild* b) {
         const int visits_a = a->to_node == nullptr ? 0 : a->to_node->visits;
         const int visits_b = b->to_node == nullptr ? 0 : b->to_node->visits;
         if (visits_a == visits_b) {
-            if (next_probability) return a->next_prob > b->next_prob;
+            if (next_probability) return node->coldOf(a).next_prob > node->coldOf(b).next_prob;
             return a->policy_prob > b->policy_prob;
         }
         return visits_a > visits_b;
@@ -200,11 +202,11 @@ Children PuctNode::sortedChildrenTraversals(const PuctNode* node, bool next_prob
     Children children;
     children.reserve(node->num_children);
     for (int ii = 0; ii < node->num_children; ii++) children.push_back(node->getNodeChild(0, ii));
-    auto f = [next_probability](const PuctNodeChild* a, const PuctNodeChild* b) {
+    auto f = [next_probability, node](const PuctNodeChild* a, const PuctNodeChild* b) {
         const int traversals_a = a->traversals;
         const int traversals_b = b->traversals;
         if (traversals_a == traversals_b) {
-            if (next_probability) return a->next_prob > b->next_prob;
+            if (next_probability) return node->coldOf(a).next_prob > node->coldOf(b).next_prob;
             return a->policy_prob > b->policy_prob;
         }
         return traversals_a > traversals_b;
@@ -240,9 +242,10 @@ void PuctNodeRequest::reply(const ModelResult& result, const GdlBasesTransformer
     const int role_count = transformer->getNumberPolicies();
     float total_prediction = 0.0f;
     const float* raw_policy = result.getPolicy(node->lead_role_index);
+    const PuctChildCold* cold = node->cold();
     for (int ii = 0; ii < node->num_children; ii++) {
         PuctNodeChild* c = node->getNodeChild(role_count, ii);
-        c->policy_prob_orig = raw_policy[c->move.get(node->lead_role_index)];
+        c->policy_prob_orig = raw_policy[cold[ii].move.get(node->lead_role_index)];
         c->policy_prob_orig = std::max(0.001f, c->policy_prob_orig);
         total_prediction += c->policy_prob_orig;
     }

@@ -16,25 +16,32 @@ typedef float Score;
 struct PuctNode;
 class GdlBasesTransformer;
 
+// A child entry is split in two records (build layout, not the reference's): the hot one holds
+// exactly what a selection pass reads -- 32 bytes, two entries per cache line -- and the cold one
+// (the joint move, the next-move probability, diagnostics) lives in a parallel array after the hot
+// array (PuctNode::cold).  Selection streams the hot array only.
 struct PuctNodeChild {
     PuctNode* to_node;
-    bool unselectable;
-    bool use_minimax;
-    uint8_t m_flags;         // mirror: kMirrorFinalised | kMirrorAllUnselectable
     uint32_t traversals;
     float policy_prob_orig;
     float policy_prob;
-    float next_prob;
-    Score debug_node_score;
-    Score debug_puct_score;
-    JointMove move;
-    // Mirror of the fields of to_node a selection pass over the parent reads (build layout, not in
-    // the reference): kept current by PuctNode::syncParent() at every change of to_node, so the
-    // selection streams the parent's child array instead of dereferencing one node per child.
-    // Valid while to_node != nullptr.
+    // Mirror of the fields of to_node a selection pass over the parent reads: kept current by
+    // PuctNode::syncParent() at every change of to_node, so the selection streams the parent's child
+    // array instead of dereferencing one node per child.  Valid while to_node != nullptr.
     Score m_score;           // to_node's current score for the parent's lead role
     uint32_t m_visits;
     uint16_t m_inflight;
+    bool unselectable;
+    uint8_t m_flags;         // mirror: kMirrorFinalised | kMirrorAllUnselectable
+};
+static_assert(sizeof(PuctNodeChild) == 32, "hot child entry: 32 bytes");
+
+struct PuctChildCold {
+    JointMove move;
+    float next_prob;
+    Score debug_node_score;
+    Score debug_puct_score;
+    bool use_minimax;
 };
 
 constexpr uint8_t kMirrorFinalised = 1, kMirrorAllUnselectable = 2;
@@ -79,14 +86,20 @@ struct PuctNode {
                                (num_children > 0 && unselectable_count == num_children ? kMirrorAllUnselectable : 0));
     }
 
-    // trailing storage: children[num_children] | final[R] | basestate words
+    // trailing storage: children[num_children] (hot) | cold[num_children] | final[R] | basestate words
     PuctNodeChild* children() { return reinterpret_cast<PuctNodeChild*>(this + 1); }
     const PuctNodeChild* children() const { return reinterpret_cast<const PuctNodeChild*>(this + 1); }
     PuctNodeChild* getNodeChild(int, int i) { return children() + i; }
     const PuctNodeChild* getNodeChild(int, int i) const { return children() + i; }
+    PuctChildCold* cold() { return reinterpret_cast<PuctChildCold*>(children() + num_children); }
+    const PuctChildCold* cold() const { return reinterpret_cast<const PuctChildCold*>(children() + num_children); }
+    // the cold record of one of this node's child entries
+    PuctChildCold& coldOf(const PuctNodeChild* c) { return cold()[c - children()]; }
+    const PuctChildCold& coldOf(const PuctNodeChild* c) const { return cold()[c - children()]; }
+    const JointMove& moveOf(const PuctNodeChild* c) const { return coldOf(c).move; }
 
-    Score* scoresPtr() { return reinterpret_cast<Score*>(children() + num_children); }
-    const Score* scoresPtr() const { return reinterpret_cast<const Score*>(children() + num_children); }
+    Score* scoresPtr() { return reinterpret_cast<Score*>(cold() + num_children); }
+    const Score* scoresPtr() const { return reinterpret_cast<const Score*>(cold() + num_children); }
 
     Score getCurrentScore(int role) const { return current[role]; }
     void setCurrentScore(int role, Score s) { current[role] = s; }

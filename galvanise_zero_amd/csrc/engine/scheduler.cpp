@@ -87,7 +87,7 @@ static void reap(std::vector<Coro*>& all, Coro* g) {
 void NetworkScheduler::prefetch_reply(int idx) const {
     const PuctNode* node = request_nodes[idx];
     const char* a = reinterpret_cast<const char*>(node);
-    const char* b = reinterpret_cast<const char*>(node->children() + node->num_children);
+    const char* b = reinterpret_cast<const char*>(node->cold() + node->num_children);   // hot + cold entries
     for (const char* q = a; q < b; q += 64) __builtin_prefetch(q, 1, 3);
     const int r = node->lead_role_index > 0 ? node->lead_role_index : 0;
     const float* pol = predict_done_event->policies[r] + (size_t)idx * transformer->getPolicySize(r);

@@ -289,10 +289,11 @@ Sample* SelfPlayManager::createSample(const PuctEvaluator* pe, const PuctNode* n
         Sample::Policy& policy = sample->policies[ri];
         for (int ii = 0; ii < node->num_children; ii++) {
             const PuctNodeChild* child = node->getNodeChild(role_count, ii);
+            const PuctChildCold& cold = node->cold()[ii];
             if (ri == node->lead_role_index) {
-                policy.emplace_back(child->move.get(ri), child->next_prob);
+                policy.emplace_back(cold.move.get(ri), cold.next_prob);
             } else {
-                policy.emplace_back(child->move.get(ri), 1.0f);
+                policy.emplace_back(cold.move.get(ri), 1.0f);
                 break;
             }
         }

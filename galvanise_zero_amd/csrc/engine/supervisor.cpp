@@ -267,7 +267,9 @@ std::tuple<int, float, int> Player::puctPlayerGetMove(int lead_role_index) {
     float probability = -1;
     const PuctNode* node = on_next_move_choice->to_node;
     if (node != nullptr) probability = node->getCurrentScore(lead_role_index);
-    return std::make_tuple(on_next_move_choice->move.get(lead_role_index), probability, evaluator->nodeCount());
+    // (the choice is a child entry of the current root: onNextMove returned it, no move applied since)
+    const JointMove& move = evaluator->getRootNode()->moveOf(on_next_move_choice);
+    return std::make_tuple(move.get(lead_role_index), probability, evaluator->nodeCount());
 }
 
 void Player::balanceNode(int max_count) {
