@@ -301,21 +301,6 @@ static inline bool travBefore(const PuctNodeChild* a, const PuctNodeChild* b) {
     return a->traversals > b->traversals;
 }
 
-// comparator of sortedChildren (node.cpp:326-339, next_probability=false)
-static inline bool visitsBefore(const PuctNodeChild* a, const PuctNodeChild* b) {
-    const int va = a->to_node == nullptr ? 0 : a->to_node->visits;
-    const int vb = b->to_node == nullptr ? 0 : b->to_node->visits;
-    if (va == vb) return a->policy_prob > b->policy_prob;
-    return va > vb;
-}
-// the same from the children's mirrors (node.h)
-static inline bool visitsBeforeM(const PuctNodeChild* a, const PuctNodeChild* b) {
-    const int va = a->to_node == nullptr ? 0 : (int)a->m_visits;
-    const int vb = b->to_node == nullptr ? 0 : (int)b->m_visits;
-    if (va == vb) return a->policy_prob > b->policy_prob;
-    return va > vb;
-}
-
 // chooseTopVisits (evaluator.cpp:1100-1136) as one unsorted pass: first win, first two non-losses
 // and first overall under travBefore, with tie flags.  add() per child, then finish().
 struct TopVisitsScan {
@@ -399,6 +384,37 @@ bool PuctEvaluator::chooseTopVisitsFast(const PuctNode* node, const PuctNodeChil
     return scan.finish(node->lead_role_index, conf->top_visits_best_guess_converge_ratio, out);
 }
 
+// the first two places under sortedChildren's comparator (node.cpp:326-339, next_probability=false:
+// visits desc, ties by policy_prob desc; M: visits from the mirrors) with their multiplicities, one
+// pass, the comparator inlined
+template <bool M>
+static void top2_visits(const PuctNodeChild* cs, int n, const PuctNodeChild** pa, int* pan,
+                        const PuctNodeChild** pb, int* pbn) {
+    auto visits = [](const PuctNodeChild* c) -> int {
+        if (c->to_node == nullptr) return 0;
+        return M ? (int)c->m_visits : (int)c->to_node->visits;
+    };
+    // before(x, y): visits desc, ties by policy_prob desc (strict)
+    const PuctNodeChild *a = cs, *b = nullptr;
+    int a_n = 1, b_n = 0, av = visits(cs), bv = 0;
+    for (int i = 1; i < n; ++i) {
+        const PuctNodeChild* c = cs + i;
+        const int cv = visits(c);
+        const float cp = c->policy_prob;
+        if (cv > av || (cv == av && cp > a->policy_prob)) {
+            b = a; b_n = a_n; bv = av;
+            a = c; a_n = 1; av = cv;
+        } else if (cv == av && !(a->policy_prob > cp)) {
+            a_n++;
+        } else if (b == nullptr || cv > bv || (cv == bv && cp > b->policy_prob)) {
+            b = c; b_n = 1; bv = cv;
+        } else if (cv == bv && !(b->policy_prob > cp)) {
+            b_n++;
+        }
+    }
+    *pa = a; *pan = a_n; *pb = b; *pbn = b_n;
+}
+
 bool PuctEvaluator::convergedFast(int count, bool* out) const {
     const int n = root->num_children;
     if (n < 2) {
@@ -407,29 +423,10 @@ bool PuctEvaluator::convergedFast(int count, bool* out) const {
     }
     // one pass: the first two places under visitsBefore with their multiplicities; both must be
     // unique for the sorted order's first two elements to be order-independent
-    const PuctNodeChild* cs = root->children();
-    const PuctNodeChild *a = nullptr, *b = nullptr;
-    int a_n = 0, b_n = 0;
-    auto before = mirror_ok ? visitsBeforeM : visitsBefore;
-    for (int i = 0; i < n; ++i) {
-        const PuctNodeChild* c = cs + i;
-        if (a == nullptr) {
-            a = c;
-            a_n = 1;
-        } else if (before(c, a)) {
-            b = a;
-            b_n = a_n;
-            a = c;
-            a_n = 1;
-        } else if (!before(a, c)) {
-            a_n++;
-        } else if (b == nullptr || before(c, b)) {
-            b = c;
-            b_n = 1;
-        } else if (!before(b, c)) {
-            b_n++;
-        }
-    }
+    const PuctNodeChild *a, *b;
+    int a_n, b_n;
+    if (mirror_ok) top2_visits<true>(root->children(), n, &a, &a_n, &b, &b_n);
+    else top2_visits<false>(root->children(), n, &a, &a_n, &b, &b_n);
     if (a_n != 1 || b == nullptr || b_n != 1) return false;
     const PuctNode* n0 = a->to_node;
     const PuctNode* n1 = b->to_node;

@@ -288,7 +288,6 @@ Sample* SelfPlayManager::createSample(const PuctEvaluator* pe, const PuctNode* n
     for (int ri = 0; ri < role_count; ri++) {
         Sample::Policy& policy = sample->policies[ri];
         for (int ii = 0; ii < node->num_children; ii++) {
-            const PuctNodeChild* child = node->getNodeChild(role_count, ii);
             const PuctChildCold& cold = node->cold()[ii];
             if (ri == node->lead_role_index) {
                 policy.emplace_back(cold.move.get(ri), cold.next_prob);
