@@ -281,3 +281,29 @@ def test_wave_group_kernel_identical_at_bench_size(n, hip_device, monkeypatch):
         outs.append(net.forward(x))
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
+
+
+def test_split_precision_against_fp32(hip_device):
+    """What the bench's dtype ("bf16x3 split") means numerically: on the bench's net and weights
+    (cfg2, random_weights(desc, 7921)) at a 1,024-row launch, the split kernel's error against the
+    float64 oracle (model.py:154-296) next to a true IEEE fp32 forward's (torch-CPU float32,
+    oracle/nn_torch.py) and the bf16 kernel's.  Measured on MI355X: profiles/r03o_precision.log.
+    The split kernel sits between the two: ~16 significant bits per operand (hi + lo bf16, lo*lo
+    dropped) against fp32's 24 and bf16's 8."""
+    from galvanise_zero_amd._native import HipNet
+    from oracle.nn_torch import TorchCPUNet
+    desc = VARIANTS["cfg2"]
+    w = random_weights(desc, 7921)
+    x = random_planes(desc, 1024, 11)
+    ref = nn_ref.forward(desc, w, x)
+    t32 = TorchCPUNet(desc, w).predict_on_batch(x)
+    errs = {"fp32 (torch-CPU)": [np.abs(np.asarray(g, np.float64) - r).max() for g, r in zip(t32, ref)]}
+    for precision in ("fp32", "bf16"):
+        net = HipNet(desc, hip_device, precision)
+        net.set_weights(to_blob(w))
+        errs["split" if precision == "fp32" else "bf16"] = [np.abs(g - r).max() for g, r in zip(net.forward(x), ref)]
+    for k, v in errs.items():
+        print("precision %-18s max |err| vs float64 oracle per output: %s" % (k, " ".join("%.3g" % e for e in v)))
+    split, f32, b16 = max(errs["split"]), max(errs["fp32 (torch-CPU)"]), max(errs["bf16"])
+    assert f32 < split < b16
+    assert split <= TOL_FP32[0] and split * 20 < b16
