@@ -56,6 +56,18 @@ public:
             row1 |= 1ull << bit(x, 1);
             rowN |= 1ull << bit(x, N);
         }
+        // lookup tables instead of divisions by the run-time N: base -> bitboard bit, square -> x / y
+        // and square -> base of each role
+        base_bit.assign(2 * N * N, 0);
+        for (int cell = 0; cell < N * N; ++cell) base_bit[2 * cell] = base_bit[2 * cell + 1] = (uint8_t)bit(cell / N + 1, cell % N + 1);
+        sq_x.assign(N * N, 0);
+        sq_y.assign(N * N, 0);
+        for (int r = 0; r < 2; ++r) sq_base[r].assign(N * N, 0);
+        for (int b = 0; b < N * N; ++b) {
+            sq_x[b] = (uint8_t)(b % N + 1);
+            sq_y[b] = (uint8_t)(b / N + 1);
+            for (int r = 0; r < 2; ++r) sq_base[r][b] = (uint16_t)cellBase(b % N + 1, b / N + 1, r);
+        }
         updateBases(init.data());
     }
 
@@ -87,10 +99,7 @@ public:
             while (word) {
                 const int b = __builtin_ctzll(word) + 64 * w;
                 word &= word - 1;
-                if (b < 2 * N * N) {
-                    const int cell = b >> 1, p = b & 1;
-                    pieces[p] |= 1ull << bit(cell / N + 1, cell % N + 1);
-                }
+                if (b < 2 * N * N) pieces[b & 1] |= 1ull << base_bit[b];
             }
         }
         mover = bs_get(bs, 2 * N * N) ? 0 : 1;
@@ -107,7 +116,7 @@ public:
         while (m) {
             const int b = __builtin_ctzll(m);
             m &= m - 1;
-            const int x = b % N + 1, y = b / N + 1, y2 = y + dy;
+            const int x = sq_x[b], y = sq_y[b], y2 = y + dy;
             if (y2 < 1 || y2 > N) continue;
             const uint64_t fwd = 1ull << bit(x, y2);
             if (!((own | opp) & fwd)) markAction(amap, fwdAction(mover, x, y));
@@ -125,6 +134,7 @@ public:
 
     int legalCount(int role) const override { return (int)legals[role].size(); }
     int legal(int role, int i) const override { return legals[role][i]; }
+    const int* legalArray(int role) const override { return legals[role].data(); }
     bool isTerminal() const override { return terminal; }
     int goalValue(int role) const override { return (role == 0 ? white_win : black_win) ? 100 : 0; }
 
@@ -145,7 +155,7 @@ public:
             while (m) {
                 const int b = __builtin_ctzll(m);
                 m &= m - 1;
-                bs_set(out, cellBase(b % N + 1, b / N + 1, role), true);
+                bs_set(out, sq_base[role][b], true);
             }
         }
         bs_set(out, 2 * N * N + next_mover, true);
@@ -174,6 +184,8 @@ private:
     std::vector<int> from_[2], to_[2];
     std::vector<uint64_t> init;
     uint64_t row1, rowN;
+    std::vector<uint8_t> base_bit, sq_x, sq_y;
+    std::vector<uint16_t> sq_base[2];
 
     // state of the last updateBases
     uint64_t pieces[2] = {0, 0};

@@ -93,6 +93,7 @@ public:
     }
     int legalCount(int r) const override { return (int)legals[r].size(); }
     int legal(int r, int i) const override { return legals[r][i]; }
+    const int* legalArray(int r) const override { return legals[r].data(); }
     bool isTerminal() const override { return terminal; }
     int goalValue(int r) const override { return goals[r]; }
 
@@ -187,6 +188,7 @@ public:
     }
     int legalCount(int r) const override { return (int)legals[r].size(); }
     int legal(int r, int i) const override { return legals[r][i]; }
+    const int* legalArray(int r) const override { return legals[r].data(); }
     bool isTerminal() const override { return black_path || white_path; }
     int goalValue(int r) const override { return (r == 0 ? black_path : white_path) ? 100 : 0; }
 
@@ -313,6 +315,7 @@ public:
     }
     int legalCount(int r) const override { return (int)legals[r].size(); }
     int legal(int r, int i) const override { return legals[r][i]; }
+    const int* legalArray(int r) const override { return legals[r].data(); }
     bool isTerminal() const override { return legals[mover].empty(); }
     int goalValue(int r) const override { return r == mover ? 0 : 100; }
 

@@ -69,31 +69,35 @@ void node_free(void* p, size_t bytes) {
 }  // namespace
 
 // node.cpp:111-149: children = cross product of every role's legal moves, role 0 outermost.
+static inline void initChild(PuctNodeChild* child, PuctChildCold* cold, const JointMove& move) {
+    child->to_node = nullptr;
+    child->unselectable = false;
+    child->m_flags = 0;
+    child->m_score = 0.0f;
+    child->m_visits = 0;
+    child->m_inflight = 0;
+    child->traversals = 0;
+    child->policy_prob_orig = 1.0f;
+    child->policy_prob = 1.0f;
+    cold->use_minimax = false;
+    cold->next_prob = 0.0f;
+    cold->debug_node_score = 0.0f;
+    cold->debug_puct_score = 0.0f;
+    cold->move = move;
+}
+
 static int initialiseChildHelper(PuctNode* node, int role_index, int child_index, int role_count,
-                                 StateMachine* sm, JointMove* joint_move) {
+                                 const int* const* legals, const int* counts, JointMove* joint_move) {
     const bool final_role = role_index == role_count - 1;
-    const int n = sm->legalCount(role_index);
+    const int n = counts[role_index];
+    const int* lg = legals[role_index];
     for (int ii = 0; ii < n; ++ii) {
-        joint_move->set(role_index, sm->legal(role_index, ii));
+        joint_move->set(role_index, lg[ii]);
         if (final_role) {
-            PuctChildCold* cold = node->cold() + child_index;
-            PuctNodeChild* child = node->getNodeChild(role_count, child_index++);
-            child->to_node = nullptr;
-            child->unselectable = false;
-            child->m_flags = 0;
-            child->m_score = 0.0f;
-            child->m_visits = 0;
-            child->m_inflight = 0;
-            child->traversals = 0;
-            child->policy_prob_orig = 1.0f;
-            child->policy_prob = 1.0f;
-            cold->use_minimax = false;
-            cold->next_prob = 0.0f;
-            cold->debug_node_score = 0.0f;
-            cold->debug_puct_score = 0.0f;
-            cold->move = *joint_move;
+            initChild(node->getNodeChild(role_count, child_index), node->cold() + child_index, *joint_move);
+            child_index++;
         } else {
-            child_index = initialiseChildHelper(node, role_index + 1, child_index, role_count, sm, joint_move);
+            child_index = initialiseChildHelper(node, role_index + 1, child_index, role_count, legals, counts, joint_move);
         }
     }
     return child_index;
@@ -154,8 +158,15 @@ PuctNode* PuctNode::create(const uint64_t* base_state, StateMachine* sm) {
     std::copy(base_state, base_state + num_words, node->getBaseState());
 
     if (!node->is_finalised) {
+        // the legal arrays once per role (not a virtual call per child)
+        const int* legals[kMaxRoles];
+        int counts[kMaxRoles];
+        for (int ri = 0; ri < role_count; ++ri) {
+            legals[ri] = sm->legalArray(ri);
+            counts[ri] = sm->legalCount(ri);
+        }
         JointMove move{};
-        const int count = initialiseChildHelper(node, 0, 0, role_count, sm, &move);
+        const int count = initialiseChildHelper(node, 0, 0, role_count, legals, counts, &move);
         (void)count;
     } else {
         for (int ii = 0; ii < role_count; ++ii) {

@@ -55,6 +55,7 @@ public:
     virtual void updateBases(const uint64_t* bs) = 0;
     virtual int legalCount(int role) const = 0;
     virtual int legal(int role, int i) const = 0;         // i-th legal action (ascending index)
+    virtual const int* legalArray(int role) const = 0;    // the legalCount(role) legal actions
     virtual bool isTerminal() const = 0;
     virtual int goalValue(int role) const = 0;            // 0..100
     virtual void nextState(const JointMove& move, uint64_t* out) = 0;
