@@ -13,10 +13,12 @@ broadcast the weight blob from rank 0 (the generation-roll hook) before timing.
 Steady state.  Every game starts from the initial position, and what a leaf costs the host depends
 on the game phase (endgames spin through up to millions of NN-free playouts per move), so a
 window right after the start measures the opening only, and no game completes in it.  The bench
-therefore first AGES the game population: it runs self-play until the population has turned over
-(--age-games: completed games per game slot, default 1.0) or --age-seconds elapse, so the timed
-window sees games of every age, as a self-play worker does after its first minutes
-(profiles/r02*_curve* show the approach to steady state).
+therefore first AGES the game population: it runs self-play until --age-games completed games per
+game slot (default 3.0) or --age-seconds (default 400) elapse.  The population starts in lockstep
+and the endgames' share of the host's time keeps growing for several generations: the 660-s curve
+of this configuration (profiles/r03p_steady_curve.log) falls from 1.33 M leaf-evals/s at one game
+per slot (120 s, the round-2 window) to ~1.04 M at three (360 s) and ~0.95 M at five (600 s), so
+the default window sits at three generations, inside the driver's time budget.
 
 A "step" = --step-rows leaf evaluations (default 2^19) per rank.  W warmup steps, then exactly K
 timed steps bracketed by barrier + synchronize; the time is the max over ranks; `value` is
@@ -60,9 +62,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--step-rows", type=int, default=1 << 19, help="leaf evaluations per step per rank")
-    ap.add_argument("--age-games", type=float, default=1.0,
+    ap.add_argument("--age-games", type=float, default=3.0,
                     help="steady state: age the game population until this many games per game slot completed ...")
-    ap.add_argument("--age-seconds", type=float, default=300.0, help="... or this many seconds passed (0: no aging)")
+    ap.add_argument("--age-seconds", type=float, default=400.0, help="... or this many seconds passed (0: no aging)")
     ap.add_argument("--threads", type=int, default=0, help="engine threads per GPU (0: the rank's CPU share - 1)")
     ap.add_argument("--pools", type=int, default=2, help="game pools per engine thread")
     ap.add_argument("--batch", type=int, default=256)
@@ -76,7 +78,7 @@ def parse():
                          "(fp32-class accuracy, the reference runs fp32 TF; default where the kernel "
                          "has it: F <= 128 on <= 8x8, F = 256 on <= 10x10); bf16 = bf16 operands "
                          "(default for cfg 4, 13x13 x 256)")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=60.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=45.0)
     ap.add_argument("--opening-seconds", type=float, default=30.0,
                     help="also report the GPU leg's rate over the first seconds of aging (the opening phase the "
                          "CPU baseline measures)")
@@ -387,10 +389,14 @@ def main():
         # the trunk kernels of small / large launches, as rocprofv3 names them (gz_net_kernel_name)
         p = 3 if args.precision == "fp32" else 1
         k_large, k_small = net.kernel_name(True), net.kernel_name(False)
-        variants = {k_large: (l_launches, l_rows, l_tms)}
-        # the same over the whole run (aging included): what a rocprofv3 summary of this command
-        # averages over
-        whole = {k_large: (s1["large_launches"], s1["large_rows"], s1["large_trunk_ms"])}
+        if k_small == k_large:   # one trunk kernel for every launch size (single-image nets)
+            variants = {k_large: (launches, rows, tms)}
+            whole = {k_large: (s1["kernel_launches"], s1["rows"], s1["trunk_ms"])}
+        else:
+            variants = {k_large: (l_launches, l_rows, l_tms)}
+            # the same over the whole run (aging included): what a rocprofv3 summary of this
+            # command averages over
+            whole = {k_large: (s1["large_launches"], s1["large_rows"], s1["large_trunk_ms"])}
         if k_small != k_large:
             variants[k_small] = (launches - l_launches, rows - l_rows, tms - l_tms)
             whole[k_small] = (s1["kernel_launches"] - s1["large_launches"], s1["rows"] - s1["large_rows"],

@@ -1127,6 +1127,9 @@ static int spin_fast_mode() {
 static bool spin_fast_enabled() { return spin_fast_mode() != 0; }
 
 static inline double spin_margin_up(double x) { return x + std::fabs(x) * 1e-6 + 1e-12; }
+// the largest policy rescaling (relative, per normalisation; twice that cumulated) an epoch's bounds
+// absorb: well inside the bounds' 1e-6 relative margin
+constexpr double kSpinDrift = 2e-7;
 static inline double spin_margin_down(double x) { return x - std::fabs(x) * 1e-6 - 1e-12; }
 
 bool PuctEvaluator::spinBuild() {
@@ -1241,8 +1244,16 @@ bool PuctEvaluator::spinBuild() {
     const double floor_adj = spin_margin_down(floor_win);
 
     uint8_t* watched = S.mark.data();
-    uint32_t v_end = (v0 / 100 + 1) * 100;   // normaliseX at the backup reaching a multiple of 100
-    for (int attempt = 0; attempt < 4; ++attempt) {
+    // Epoch length.  The bounds read the children's policies, which change at normaliseX (every
+    // 100 root visits).  Deep in a spin that rescales every policy by 1 / total with total within
+    // a few float ulps of 1 (the wins sit below their decay minimum), and the spin loops re-check
+    // the factor at each normalisation, ending the epoch when it drifts (kSpinDrift): so a long
+    // epoch (16 normalisations) is tried first and taken when it leaves every non-win unwatched;
+    // otherwise the epoch ends at the next normalisation, shortened until the watched set fits.
+    const uint32_t v_next100 = (v0 / 100 + 1) * 100;
+    uint32_t v_end = v_next100 + 1500;
+    bool long_try = true;
+    for (int attempt = 0; attempt < 5; ++attempt) {
         const uint32_t vl = v_end - 1;         // the epoch's last selection
         const float pc = pc_at(vl);
         const double sq = std::sqrt(vl + 1);
@@ -1269,6 +1280,13 @@ bool PuctEvaluator::spinBuild() {
             } else {
                 spin.watched_flag[nwatch++] = (uint16_t)i;
                 watch_prior = watch_prior || kind[i] == kUnexp;
+            }
+        }
+        if (long_try) {
+            long_try = false;
+            if (!ok || nwatch != 0) {
+                v_end = v_next100;
+                continue;
             }
         }
         if (ok) {
@@ -1304,6 +1322,7 @@ bool PuctEvaluator::spinBuild() {
             spin.root = node;
             spin.v_end = v_end;
             spin.reach = reach;
+            spin.drift = 1.0;
             spin.valid = true;
             return true;
         }
@@ -1386,6 +1405,8 @@ PuctEvaluator::SpinSnapshot PuctEvaluator::spinSnapshot() const {
     for (int k = 0; k < spin.ncand; ++k) add(cs[spin.cand[k]].to_node);
     s.valid = spin.valid;
     s.fail_next = spin.fail_next;
+    s.v_end = spin.v_end;
+    s.drift = spin.drift;
     s.rng = rng;
     s.playouts_finals = stats.playouts_finals;
     s.num_tree_playouts = stats.num_tree_playouts;
@@ -1405,6 +1426,8 @@ void PuctEvaluator::spinRestore(const SpinSnapshot& s) {
     for (int k = 0; k < spin.ncand; ++k) put(cs[spin.cand[k]].to_node);
     spin.valid = s.valid;
     spin.fail_next = s.fail_next;
+    spin.v_end = s.v_end;
+    spin.drift = s.drift;
     rng = s.rng;
     stats.playouts_finals = s.playouts_finals;
     stats.num_tree_playouts = s.num_tree_playouts;
@@ -1412,7 +1435,8 @@ void PuctEvaluator::spinRestore(const SpinSnapshot& s) {
 }
 
 bool PuctEvaluator::SpinSnapshot::operator==(const SpinSnapshot& o) const {
-    return bytes == o.bytes && valid == o.valid && fail_next == o.fail_next && rng == o.rng &&
+    return bytes == o.bytes && valid == o.valid && fail_next == o.fail_next && v_end == o.v_end &&
+           drift == o.drift && rng == o.rng &&
            playouts_finals == o.playouts_finals && num_tree_playouts == o.num_tree_playouts &&
            total_tree_playouts == o.total_tree_playouts;
 }
@@ -1559,7 +1583,17 @@ int PuctEvaluator::spinRunSlow(int limit, bool verify) {
                 chosen->policy_prob = std::max(minimum, chosen->policy_prob);
             }
         }
-        if (node->visits % 100 == 0) node->normaliseX();
+        if (node->visits % 100 == 0) {
+            // normaliseX inside an epoch: the epoch expires when the rescaling drifts (spinBuild)
+            float before[SpinEpoch::kMaxWins + SpinEpoch::kMaxWatched];
+            for (int k = 0; k < spin.ncand; ++k) before[k] = cs[spin.cand[k]].policy_prob;
+            node->normaliseX();
+            double dev = 0.0;
+            for (int k = 0; k < spin.ncand; ++k)
+                dev = std::max(dev, std::fabs((double)cs[spin.cand[k]].policy_prob / (double)before[k] - 1.0));
+            spin.drift *= (double)cs[spin.cand[0]].policy_prob / (double)before[0];
+            if (dev > kSpinDrift || std::fabs(spin.drift - 1.0) > 2 * kSpinDrift) spin.v_end = node->visits;
+        }
         stats.num_tree_playouts++;
         total_tree_playouts++;
         ++done;
@@ -1595,7 +1629,32 @@ struct SpinRegs {
     uint32_t touched = 0;   // candidates chosen in this run (bit k)
     int done = 0;
     bool failed = false;
+    PuctNode* node = nullptr;        // the root (normaliseX inside a run)
+    const uint16_t* cand = nullptr;  // candidate k's child index
+    double drift = 1.0;              // the epoch's product of normalisation factors
+    bool expired = false;            // a normalisation drifted: the epoch ends after this playout
 };
+
+// normaliseX at the root inside a register run (backup, evaluator.cpp:650): the candidates'
+// policies to the child entries, normalise, read them back; the epoch expires when the factor
+// drifts (spinBuild's bounds assume the policies it read, within kSpinDrift)
+inline void spin_normalise(SpinRegs& x, float* P, int nc) {
+    PuctNodeChild* cs = x.node->children();
+    float before[SpinRegs::kC];
+    for (int k = 0; k < nc; ++k) {
+        before[k] = P[k];
+        cs[x.cand[k]].policy_prob = P[k];
+    }
+    x.node->normaliseX();
+    double dev = 0.0;
+    for (int k = 0; k < nc; ++k) {
+        P[k] = cs[x.cand[k]].policy_prob;
+        dev = std::max(dev, std::fabs((double)P[k] / (double)before[k] - 1.0));
+    }
+    x.drift *= (double)P[0] / (double)before[0];
+    x.touched = (1u << nc) - 1;
+    if (dev > kSpinDrift || std::fabs(x.drift - 1.0) > 2 * kSpinDrift) x.expired = true;
+}
 
 // backup()'s policy decay of the chosen child at the root (evaluator.cpp:605-625)
 inline void decay_params(float cur_score, float* apply, float* minimum) {
@@ -1700,6 +1759,10 @@ __attribute__((noinline)) void spin_wins(SpinRegs& x, int limit) {
             P[k] = ch && dec && p > minimum ? pn : p;
         }
         ++done;
+        if (v % 100 == 0) {
+            spin_normalise(x, P, NC);
+            if (x.expired) break;
+        }
     }
     for (int k = 0; k < NC; ++k) { x.P[k] = P[k]; x.T[k] = T[k]; x.LV[k] = LV[k]; }
     for (int ii = 0; ii < R; ii++) x.cur[ii] = cur[ii];
@@ -1771,6 +1834,10 @@ void spin_mixed(SpinRegs& x, int limit) {
             }
         }
         ++x.done;
+        if (x.v % 100 == 0) {
+            spin_normalise(x, x.P, nc);
+            if (x.expired) break;
+        }
     }
 }
 }  // namespace
@@ -1812,6 +1879,9 @@ int PuctEvaluator::spinRunRegs(int limit) {
     x.v = node->visits;
     x.v_end = spin.v_end;
     x.reach = (uint64_t)spin.reach;
+    x.node = node;
+    x.cand = spin.cand;
+    x.drift = spin.drift;
     if (all_win && x.role_count == 2 && nc == 2) spin_wins<2, 2>(x, limit);
     else if (all_win && x.role_count == 2 && nc == 3) spin_wins<3, 2>(x, limit);
     else if (all_win && x.role_count == 2 && nc == 4) spin_wins<4, 2>(x, limit);
@@ -1827,11 +1897,12 @@ int PuctEvaluator::spinRunRegs(int limit) {
         c->to_node->visits = x.LV[k];
         c->to_node->syncParent();
     }
+    spin.drift = x.drift;
+    if (x.expired) spin.v_end = x.v;   // the next call rebuilds the epoch
     if (done > 0) {
         node->visits = x.v;
         for (int ii = 0; ii < x.role_count; ii++) node->setCurrentScore(ii, x.cur[ii]);
         node->syncParent();
-        if (x.v % 100 == 0) node->normaliseX();   // only at v_end (spinBuild)
         stats.playouts_finals += done;
         stats.num_tree_playouts += done;
         total_tree_playouts += done;

@@ -121,6 +121,7 @@ private:
         bool valid = false;
         bool fail_next = false;      // spinRun: the next playout fails the fast path (seen in the last run)
         bool regs_ok = false;        // spinRunRegs applies: no watched prior, every win a childless leaf
+        double drift = 1.0;          // product of the policy rescalings (normaliseX) since the build
     };
     bool spinBuild();
     int spinRun(int limit, bool multi);
@@ -129,6 +130,8 @@ private:
     struct SpinSnapshot {
         std::vector<char> bytes;
         bool valid = false, fail_next = false;
+        uint32_t v_end = 0;
+        double drift = 1.0;
         Rng rng;
         int playouts_finals = 0, num_tree_playouts = 0;
         long total_tree_playouts = 0;

@@ -11,6 +11,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def rss_gb():
+    try:
+        with open("/proc/self/status") as f:
+            for line in f:
+                if line.startswith("VmRSS:"):
+                    return int(line.split()[1]) / 1e6
+    except OSError:
+        pass
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=300)
@@ -50,6 +61,9 @@ def main():
                "games_total": st["games_completed"], "games_per_slot": st["games_completed"] / games,
                "gpu_busy": d["kernel_ms"] / 1e3 / dt,
                "rows_per_launch": d["rows"] / max(1, d["kernel_launches"]),
+               "nn_free_playouts_per_leaf": (d["tree_playouts"] - d["rows"]) / max(1, d["rows"]),
+               "engine_idle": d["engine_idle_ms"] / 1e3 / dt / threads,
+               "rss_gb": rss_gb(),
                "evals_per_game_cum": st["completed_game_evals"] / max(1, st["games_completed"])}
         rows_log.append(row)
         print(json.dumps(row), flush=True)
