@@ -48,11 +48,11 @@ NUM_CUS = 256
 # run, so the figure measured for the same kernel is reported with its source.
 TRAFFIC_PER_LAUNCH = {"gznn::trunk_kernel<128, 4, 1, 1, 1>": (14290.1 * 2 + 320.0) * 1024,
                       "gznn::trunk_kernel<128, 4, 2, 1, 1>": (14722.3 * 2 + 800.0) * 1024,
-                      "gznn::trunk_kernel<128, 4, 2, 1, 3>": (59483.6 * 2 + 1280.0) * 1024}
+                      "gznn::trunk_kernel<128, 4, 2, 1, 3>": (58444.6 * 2 + 1280.0) * 1024}
 TRAFFIC_SOURCE = {
     "gznn::trunk_kernel<128, 4, 1, 1, 1>": "profiles/r01k_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 256-row launches)",
     "gznn::trunk_kernel<128, 4, 2, 1, 1>": "profiles/r01k_pmc.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, 640-row launches)",
-    "gznn::trunk_kernel<128, 4, 2, 1, 3>": "profiles/r02r_pmc_fp32_1024rows.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+    "gznn::trunk_kernel<128, 4, 2, 1, 3>": "profiles/r03r_pmc_summary.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                                            "separate passes, 1024-row launches; FETCH x2 gfx950 correction, 1 KB units)"}
 
 

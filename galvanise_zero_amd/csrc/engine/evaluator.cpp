@@ -56,6 +56,33 @@ static inline float puct_log(uint32_t visits) {
 }
 
 
+// GZ_SPIN_STATS=1: spin fast-path counters (process totals, printed at exit; diagnostics only)
+namespace {
+enum SpinStat {
+    kSdBuilds, kSdBuildOk, kSdFailRoot, kSdFailUnselectable, kSdFailVisited, kSdFailInflight, kSdFailWinNode,
+    kSdFailWinScore, kSdFailLatch, kSdFailFewWins, kSdFailOrder, kSdFailWatched, kSdRegsPlayouts,
+    kSdSlowPlayouts, kSdOrdinaryPlayouts, kSdRetryWait, kSdSelect, kSdSelectSorted, kSdCount
+};
+struct SpinStats {
+    const bool on = std::getenv("GZ_SPIN_STATS") != nullptr;
+    std::atomic<long> c[kSdCount] = {};
+    ~SpinStats() {
+        if (!on) return;
+        static const char* names[kSdCount] = {
+            "builds", "build_ok", "fail_root", "fail_unselectable", "fail_visited", "fail_inflight",
+            "fail_win_node", "fail_win_score", "fail_latch", "fail_few_wins", "fail_order", "fail_watched",
+            "regs_playouts", "slow_playouts", "ordinary_playouts", "retry_wait", "select", "select_sorted"};
+        std::fprintf(stderr, "gz spin stats:");
+        for (int i = 0; i < kSdCount; ++i) std::fprintf(stderr, " %s=%ld", names[i], c[i].load());
+        std::fprintf(stderr, "\n");
+    }
+};
+SpinStats g_spin_stats;
+inline void sd(SpinStat i, long n = 1) {
+    if (__builtin_expect(g_spin_stats.on, 0)) g_spin_stats.c[i].fetch_add(n, std::memory_order_relaxed);
+}
+}  // namespace
+
 #define GZ_ASSERT(cond)                                                                     \
     do {                                                                                    \
         if (!(cond)) {                                                                      \
@@ -852,7 +879,9 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
     }
 
     // 2. the reference's loop in sorted order over the gathered terms
+    sd(kSdSelect);
     if (!done) {
+        sd(kSdSelectSorted);
         const uint16_t* order = S.sortedOrder(n);
         float best_score = -1;
         PuctNodeChild* best_child = nullptr;
@@ -1089,32 +1118,6 @@ int PuctEvaluator::treePlayout(PuctNode* current, Path& path) {
 // the result stands when it is a win and beats every unwatched bound with margin (unwatched
 // elements below the final best cannot change the loop's outcome).
 
-// GZ_SPIN_STATS=1: spin fast-path counters (process totals, printed at exit; diagnostics only)
-namespace {
-enum SpinStat {
-    kSdBuilds, kSdBuildOk, kSdFailRoot, kSdFailUnselectable, kSdFailVisited, kSdFailInflight, kSdFailWinNode,
-    kSdFailWinScore, kSdFailLatch, kSdFailFewWins, kSdFailOrder, kSdFailWatched, kSdRegsPlayouts,
-    kSdSlowPlayouts, kSdOrdinaryPlayouts, kSdRetryWait, kSdCount
-};
-struct SpinStats {
-    const bool on = std::getenv("GZ_SPIN_STATS") != nullptr;
-    std::atomic<long> c[kSdCount] = {};
-    ~SpinStats() {
-        if (!on) return;
-        static const char* names[kSdCount] = {
-            "builds", "build_ok", "fail_root", "fail_unselectable", "fail_visited", "fail_inflight",
-            "fail_win_node", "fail_win_score", "fail_latch", "fail_few_wins", "fail_order", "fail_watched",
-            "regs_playouts", "slow_playouts", "ordinary_playouts", "retry_wait"};
-        std::fprintf(stderr, "gz spin stats:");
-        for (int i = 0; i < kSdCount; ++i) std::fprintf(stderr, " %s=%ld", names[i], c[i].load());
-        std::fprintf(stderr, "\n");
-    }
-};
-SpinStats g_spin_stats;
-inline void sd(SpinStat i, long n = 1) {
-    if (__builtin_expect(g_spin_stats.on, 0)) g_spin_stats.c[i].fetch_add(n, std::memory_order_relaxed);
-}
-}  // namespace
 
 // GZ_SPIN_FAST=0: no spin fast path; =2: the fast path without spinRunRegs (tests compare all three)
 static int spin_fast_mode() {
