@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <immintrin.h>
 #include <limits>
 #include <mutex>
 #include <random>
@@ -54,6 +55,26 @@ static inline float puct_log(uint32_t visits) {
     if (__builtin_expect(t == nullptr, 0)) t = puct_log_block(b);
     return t[visits & ((1u << kPuctLogBlockBits) - 1)];
 }
+
+// puct_log at consecutive visit counts (a spin run): the current 64K block held, refreshed at its end
+struct PuctLogCursor {
+    const float* t = nullptr;
+    uint32_t b = ~0u;
+    inline float at(uint32_t visits) {
+        const uint32_t vb = visits >> kPuctLogBlockBits;
+        if (__builtin_expect(vb != b, 0)) {
+            if (vb >= (uint32_t)kPuctLogBlocks) return puct_log_direct(visits);
+            t = g_puct_log[vb].load(std::memory_order_acquire);
+            if (t == nullptr) t = puct_log_block(vb);
+            b = vb;
+        }
+        return t[visits & ((1u << kPuctLogBlockBits) - 1)];
+    }
+};
+
+// sqrt of a positive double as the one sqrtsd instruction (std::sqrt adds a domain check for errno;
+// the result is the same correctly rounded value)
+static inline double sqrt_pos(double x) { return _mm_cvtsd_f64(_mm_sqrt_sd(_mm_setzero_pd(), _mm_set_sd(x))); }
 
 
 // GZ_SPIN_STATS=1: spin fast-path counters (process totals, printed at exit; diagnostics only)
@@ -1704,20 +1725,31 @@ __attribute__((noinline)) void spin_wins(SpinRegs& x, int limit) {
     uint64_t discards = 0;
     int done = 0;
     bool failed = false;
+    PuctLogCursor plog;
+    // a win reaches the root latch only when its traversals exceed 0.66 v: over this run a win's
+    // traversals grow by at most the run's length while v only grows, so when even that cannot
+    // reach 0.66 v (with a margin far above the float rounding of both sides) no playout of the run
+    // needs the check
+    uint32_t tmax = 0;
+    for (int k = 0; k < NC; ++k) tmax = std::max(tmax, T[k]);
+    const uint32_t run_max = std::min<uint32_t>((uint32_t)std::max(limit, 0), v_end - v);
+    const bool check_latch = !((double)tmax + run_max < 0.66 * (double)v * (1.0 - 1e-5));
     while (done < limit && v < v_end) {
         if (noise_check && lead_score(cur) <= 0.95) {
             failed = true;
             break;
         }
-        pc = puct_log(v);
+        pc = plog.at(v);
         pc += pc_root;
-        const double sqrt_node_visits = std::sqrt(v + 1);
+        const double sqrt_node_visits = sqrt_pos(v + 1);
         const bool latch = v > 1000 && v < 40000000;
-        bool latched_win = false;
-        for (int k = 0; k < NC; ++k) latched_win |= T[k] > 16 && T[k] > v * limit_latch_root;
-        if (latch && latched_win) {
-            failed = true;
-            break;
+        if (check_latch) {
+            bool latched_win = false;
+            for (int k = 0; k < NC; ++k) latched_win |= T[k] > 16 && T[k] > v * limit_latch_root;
+            if (latch && latched_win) {
+                failed = true;
+                break;
+            }
         }
         double child_score = win_base;
         child_score *= 1.0f + pc;
