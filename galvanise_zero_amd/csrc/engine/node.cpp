@@ -6,6 +6,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <limits>
+#include <mutex>
+
+#include <sys/mman.h>
 
 namespace gz {
 
@@ -20,51 +23,92 @@ static size_t node_bytes(int num_children, int role_count, int num_words) {
 }
 
 // Node memory: nodes are variable-size (children count) and the tree churns through them (every
-// expansion allocates one, every move releases the siblings' subtrees).  A per-thread cache of freed
-// blocks per 64-byte size class recycles them without going through malloc's free lists (whose
-// unlink checks touched cold neighbouring chunks: ~5 % of engine time).  A game's nodes are created
-// and released on the engine thread that polls its pool; a block freed on another thread simply
-// joins that thread's cache.  Cached blocks are returned to the system when the thread exits, or at
-// once beyond kNodeCacheBytes per thread.
+// expansion allocates one, every move releases the siblings' subtrees).  Nodes of up to 64 KiB are
+// carved from 2 MiB chunks advised as transparent huge pages (a bench runner holds ~14 GB of trees:
+// with 4 KiB pages nearly every cold node visit is also a TLB miss) and recycled per thread by
+// 64-byte size class, without malloc's free lists (whose unlink checks touched cold neighbouring
+// chunks: ~5 % of engine time).  A block freed on another thread joins that thread's lists; a
+// thread's lists pass to a process-wide pool when it exits, and new blocks come from that pool
+// before a fresh chunk.  Chunks live as long as the process; larger nodes use aligned_alloc.
 namespace {
-constexpr size_t kNodeCacheBytes = size_t(256) << 20;
-constexpr size_t kNodeCacheClasses = 1024;     // blocks up to 64 KiB are cached
+constexpr size_t kNodeCacheClasses = 1024;     // blocks up to 64 KiB come from chunks
+constexpr size_t kChunkBytes = size_t(2) << 20;
+
+struct NodePool {   // process-wide: blocks of exited threads, per size class
+    std::mutex mu;
+    void* head[kNodeCacheClasses] = {};
+};
+NodePool& node_pool() {
+    static NodePool* p = new NodePool();   // never destroyed (threads may exit during static teardown)
+    return *p;
+}
+
 struct NodeCache {
     void* head[kNodeCacheClasses] = {};
-    size_t bytes = 0;
+    char* cur = nullptr;   // bump region of the current chunk
+    char* end = nullptr;
     ~NodeCache() {
-        for (size_t c = 0; c < kNodeCacheClasses; ++c)
-            for (void* p = head[c]; p != nullptr;) {
-                void* next = *static_cast<void**>(p);
-                std::free(p);
-                p = next;
-            }
+        NodePool& pool = node_pool();
+        std::lock_guard<std::mutex> lk(pool.mu);
+        for (size_t c = 0; c < kNodeCacheClasses; ++c) {
+            void* p = head[c];
+            if (p == nullptr) continue;
+            void* last = p;
+            while (*static_cast<void**>(last) != nullptr) last = *static_cast<void**>(last);
+            *static_cast<void**>(last) = pool.head[c];
+            pool.head[c] = p;
+        }
+    }
+    void* fresh(size_t bytes) {
+        if (cur == nullptr || (size_t)(end - cur) < bytes) {
+            void* chunk = std::aligned_alloc(kChunkBytes, kChunkBytes);
+            if (chunk == nullptr) return nullptr;
+            madvise(chunk, kChunkBytes, MADV_HUGEPAGE);   // advice only: 4 KiB pages if refused
+            cur = static_cast<char*>(chunk);
+            end = cur + kChunkBytes;
+        }
+        void* p = cur;
+        cur += bytes;
+        return p;
     }
 };
 
+#if defined(__SANITIZE_ADDRESS__)
+// AddressSanitizer builds (tests/test_transpositions.py): every node through malloc, so a use
+// after free is caught instead of landing in a recycled block
+constexpr bool kPooled = false;
+#else
+constexpr bool kPooled = true;
+#endif
+
 void* node_alloc(size_t bytes) {   // bytes: a multiple of 64
     const size_t c = bytes / 64;
-    if (c < kNodeCacheClasses) {
-        NodeCache& nc = tls_instance<NodeCache>();
-        if (void* p = nc.head[c]) {
-            nc.head[c] = *static_cast<void**>(p);
-            nc.bytes -= bytes;
+    if (!kPooled || c >= kNodeCacheClasses) return std::aligned_alloc(64, bytes);
+    NodeCache& nc = tls_instance<NodeCache>();
+    if (void* p = nc.head[c]) {
+        nc.head[c] = *static_cast<void**>(p);
+        return p;
+    }
+    {   // blocks of exited threads
+        NodePool& pool = node_pool();
+        std::lock_guard<std::mutex> lk(pool.mu);
+        if (void* p = pool.head[c]) {
+            pool.head[c] = *static_cast<void**>(p);
             return p;
         }
     }
-    return std::aligned_alloc(64, bytes);
+    return nc.fresh(bytes);
 }
 
 void node_free(void* p, size_t bytes) {
     const size_t c = bytes / 64;
-    NodeCache& nc = tls_instance<NodeCache>();
-    if (c < kNodeCacheClasses && nc.bytes + bytes <= kNodeCacheBytes) {
-        *static_cast<void**>(p) = nc.head[c];
-        nc.head[c] = p;
-        nc.bytes += bytes;
+    if (!kPooled || c >= kNodeCacheClasses) {
+        std::free(p);
         return;
     }
-    std::free(p);
+    NodeCache& nc = tls_instance<NodeCache>();
+    *static_cast<void**>(p) = nc.head[c];
+    nc.head[c] = p;
 }
 }  // namespace
 
