@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--age-games", type=float, default=3.0,
                     help="steady state: age the game population until this many games per game slot completed ...")
     ap.add_argument("--age-seconds", type=float, default=400.0, help="... or this many seconds passed (0: no aging)")
-    ap.add_argument("--threads", type=int, default=0, help="engine threads per GPU (0: the rank's CPU share - 1)")
+    ap.add_argument("--threads", type=int, default=0, help="engine threads per GPU (0: the rank's CPU share)")
     ap.add_argument("--pools", type=int, default=2, help="game pools per engine thread")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--evals", type=int, default=0, help="evals per move (0: the config's, 800 for cfg2)")
@@ -292,7 +292,10 @@ def main():
     net.set_weights_device(blob.data_ptr(), net.weight_count)
     blob_sum = float(blob.double().sum().item())
 
-    threads = args.threads or max(1, cpus - 1)   # + the launcher (mostly asleep) and main
+    # one engine thread per CPU of the rank's share (the launcher and main threads mostly sleep):
+    # on the 16-CPU box 16 threads ran 13-18 % faster than 15; 20 about 3 % more at 56 % engine idle
+    # (quota throttling), 24 slower (profiles/r03t_bench_threads*.log, r03u_bench_threads.txt)
+    threads = args.threads or max(1, cpus)
     games_per_rank = threads * args.pools * args.batch
     game_base = shard.game_index_base(rank, games_per_rank)
     runner = SelfPlayRunner(net, sm, transformer, selfplay_conf(args.mode, evals), device=device,

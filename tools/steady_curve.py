@@ -42,7 +42,7 @@ def main():
     # the bench's network: bf16x3 split where compiled, the bench's weights
     net = HipNet(desc, 0, "fp32" if desc.cnn_filter_size <= 128 or desc.hw <= 112 else "bf16")
     net.set_weights(to_blob(random_weights(desc, 7921)))
-    threads = args.threads or max(1, bench.cpu_share() - 1)   # as bench.py (cgroup quota aware)
+    threads = args.threads or max(1, bench.cpu_share())   # as bench.py (cgroup quota aware)
     conf = bench.selfplay_conf("template", BASELINE_CONFIGS[args.config]["evals"])
     r = SelfPlayRunner(net, sm, t, conf, device=0, num_threads=threads, pools_per_thread=args.pools,
                        batch_size=args.batch, seed=20251015, spin_yield_playouts=args.spin_yield,
