@@ -75,9 +75,8 @@ def parse():
     ap.add_argument("--mode", choices=["template", "literal"], default="template")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
                     help="trunk arithmetic: fp32 = split hi/lo bf16 operands, three MFMAs per product "
-                         "(fp32-class accuracy, the reference runs fp32 TF; default where the kernel "
-                         "has it: F <= 128 on <= 8x8, F = 256 on <= 10x10); bf16 = bf16 operands "
-                         "(default for cfg 4, 13x13 x 256)")
+                         "(fp32-class accuracy, the reference runs fp32 TF; the default, every config); "
+                         "bf16 = bf16 operands")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=45.0)
     ap.add_argument("--opening-seconds", type=float, default=30.0,
                     help="also report the GPU leg's rate over the first seconds of aging (the opening phase the "
@@ -277,9 +276,8 @@ def main():
     evals = args.evals or BASELINE_CONFIGS[args.config]["evals"]
     sm, transformer, desc = setup_game(args.config)
     if args.precision is None:
-        # bf16x3 split wherever it is compiled: F <= 128 on boards <= 64 positions, F = 256 on boards
-        # <= 112 positions (single image); hexLG13's 12 x 256 on 13 x 13 (cfg 4) runs bf16
-        args.precision = "fp32" if desc.cnn_filter_size <= 128 or desc.hw <= 112 else "bf16"
+        # bf16x3 split on every BASELINE config (F = 256 on 13 x 13, cfg 4: the two-pass kernel)
+        args.precision = "fp32"
     net = HipNet(desc, device, args.precision)
     heads_fused = net.heads_fused()
 

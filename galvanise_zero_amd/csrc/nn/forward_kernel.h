@@ -140,11 +140,17 @@ __host__ __device__ constexpr int lcm_c(int a, int b) { return a / gcd_c(a, b) *
 // P = 1: bf16 operands.  P = 3: split precision ("fp32 accuracy"): every fp32 operand x is carried
 // as x_hi = bf16(x), x_lo = bf16(x - x_hi) and each product as hi*hi + hi*lo + lo*hi (three MFMAs,
 // fp32 accumulation): ~16 significant bits per operand instead of 8.
+// P = 2: the same split products for single-image kernels whose hi + lo image exceeds the LDS
+// (F = 256 on 13 x 13): the LDS image holds one part at a time.  Each conv runs two passes over the
+// same weight stages: pass 0 over the hi image (W_hi x_hi + W_lo x_hi), then the lo image is copied
+// in from a per-workgroup device scratch (written by the previous epilogue) and pass 1 adds
+// W_hi x_lo.
 // WG = wave groups per workgroup: 1 (4 waves for NB boards) or 2 (8 waves, 2 per SIMD: group g takes
 // board g of the workgroup with NB = 1; the register budget is then 256 per wave)
 template <int F, int PTN, int NB = 1, int P = 1, int WG = 1>
 struct Geo {
-    static constexpr int P2 = P == 3 ? 2 : 1;        // bf16 parts per operand
+    static constexpr int P2 = P == 3 ? 2 : 1;        // bf16 parts per activation in the LDS image
+    static constexpr int WP = P == 1 ? 1 : 2;        // bf16 parts per weight
     // the board (H x W, runtime: kp.H / kp.W) has at most NPOS = 16 * PTN positions
     static constexpr int NPOS = 16 * PTN;            // position capacity (the real count is kp.npos)
     static constexpr int PT = PTN;                   // position tiles per board (MFMA N)
@@ -175,9 +181,9 @@ struct Geo {
     // k-steps per ring stage and the ring's VGPR budget: F = 256 (4 co tiles per wave, 16 weight
     // VGPRs per k-step) streams single k-steps through a 64-VGPR ring so the accumulators, the
     // residual and the B fragments still fit the 512 registers of a wave without spilling
-    static constexpr int KS = (CT >= 4 || P2 == 2) ? 1 : 2;
-    static constexpr int NFR = CT * P2;              // weight fragments per k-step per lane
-    static constexpr int ROWB = 64 * P2;             // bytes per output channel per k-step
+    static constexpr int KS = (CT >= 4 || WP == 2) ? 1 : 2;
+    static constexpr int NFR = CT * WP;              // weight fragments per k-step per lane
+    static constexpr int ROWB = 64 * WP;             // bytes per output channel per k-step
     static constexpr int NST = 9 * KC / KS;          // ring stages per conv
     // ring depth; the two-board split kernels take exactly one tap's stages (R = KC / KS) so the
     // looped conv's body is one tap (a deeper ring made the body three taps and spilled)
@@ -209,6 +215,8 @@ struct Geo {
     static_assert(WG == 1 || (NB == 1 && !SI), "wave groups: one board per group, two images");
     static_assert(!RG || SI, "the global residual is implemented for single-image kernels");
     static constexpr int RESID_BYTES = RG ? 4 * CT * TT * 64 * 16 : 0;   // per workgroup
+    // P = 2: the lo image of each workgroup (device scratch after the grid's residual scratch)
+    static constexpr int LO_BYTES = P == 2 ? ACT_BYTES : 0;
     static_assert(KC % KS == 0, "a stage must not straddle a tap");
     static_assert(R >= 2, "no ring depth fits");
     // Looped conv (two-image kernels): the 9-tap conv runs as NIT iterations of a body of U ring
@@ -258,7 +266,8 @@ __device__ __forceinline__ float bf16_lo(float x) { return x - (float)(__bf16)x;
 
 // SEL: off-board lanes of a partial last tile write the scratch row (a select, not a branch: the
 // two-image kernels); otherwise they branch around the store (single-image kernels, whose 40+ tile
-// epilogues keep fewer values live that way)
+// epilogues keep fewer values live that way).  P = 2: the lo parts (the epilogue's first image; the
+// workgroup saves it to device memory and then writes the hi parts, save_lo_write_hi).
 template <int F, int PTN, int P = 1, bool SEL = true>
 __device__ __forceinline__ void store_act(char* X, int p, int co, f32x4 v, int npos) {
     using G = Geo<F, PTN, 1, P>;
@@ -267,8 +276,13 @@ __device__ __forceinline__ void store_act(char* X, int p, int co, f32x4 v, int n
         const int chunk = G::WRAP ? (co >> 3) : ((co >> 3) + swz(q));
         char* a = X + q * G::ROWS + (chunk << 4) + (co & 7) * 2;
         uint2 u;
-        u.x = pack2(v[0], v[1]);
-        u.y = pack2(v[2], v[3]);
+        if constexpr (P == 2) {
+            u.x = pack2(bf16_lo(v[0]), bf16_lo(v[1]));
+            u.y = pack2(bf16_lo(v[2]), bf16_lo(v[3]));
+        } else {
+            u.x = pack2(v[0], v[1]);
+            u.y = pack2(v[2], v[3]);
+        }
         *(uint2*)a = u;
         if constexpr (G::P2 == 2) {    // the lo part, same chunk of the row's second half
             uint2 l;
@@ -316,7 +330,7 @@ __device__ __forceinline__ void ring_ready(bf16x8& v) { asm volatile("" : "+v"(v
 template <int F, int PTN, int NB, int P, int WG = 1>
 struct Ring {
     using G = Geo<F, PTN, NB, P, WG>;
-    bf16x8 r[G::R][G::KS][G::NFR];    // fragment f = ct * P2 + part
+    bf16x8 r[G::R][G::KS][G::NFR];    // fragment f = ct * WP + part
 };
 
 // Issue stage `gs` of the trunk weight stream (clamped to the last stage) into ring slot SLOT.
@@ -326,24 +340,27 @@ struct Ring {
 // copies values between VGPRs and AGPRs freely: an inline-asm load's destination could be copied
 // (or its register reused) before the data lands.  They issue the ring with ordinary loads, which
 // the compiler tracks (it places the waits and never copies an in-flight register).
-// byte offset of weight fragment f (= ct * P2 + part) within a k-step, relative to the lane's row
-template <int P2, int ROWB, int FR>
+// byte offset of weight fragment f (= ct * WP + part) within a k-step, relative to the lane's row
+template <int WP, int ROWB, int FR>
 struct FragOff {
-    static constexpr int value = (FR / P2) * 16 * ROWB + (FR % P2) * 64;
+    static constexpr int value = (FR / WP) * 16 * ROWB + (FR % WP) * 64;
 };
 template <int F, int PTN, int NB, int P, int WG, int SLOT, int... FRS>
 __device__ __forceinline__ void ring_issue_k(Ring<F, PTN, NB, P, WG>& ring, int k, uint32_t woff, const char* sb,
                                              std::integer_sequence<int, FRS...>) {
     using G = Geo<F, PTN, NB, P, WG>;
     if constexpr (G::TRACKED)
-        ((ring.r[SLOT][k][FRS] = *(const bf16x8*)(sb + woff + FragOff<G::P2, G::ROWB, FRS>::value)), ...);
+        ((ring.r[SLOT][k][FRS] = *(const bf16x8*)(sb + woff + FragOff<G::WP, G::ROWB, FRS>::value)), ...);
     else
-        ((ring.r[SLOT][k][FRS] = gload_issue<FragOff<G::P2, G::ROWB, FRS>::value>(woff, sb)), ...);
+        ((ring.r[SLOT][k][FRS] = gload_issue<FragOff<G::WP, G::ROWB, FRS>::value>(woff, sb)), ...);
 }
 template <int F, int PTN, int NB, int P, int WG, int SLOT>
 __device__ __forceinline__ void ring_issue(Ring<F, PTN, NB, P, WG>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
     using G = Geo<F, PTN, NB, P, WG>;
-    const int s = gs < gmax ? gs : gmax;
+    int s = gs < gmax ? gs : gmax;
+    // P = 2: global stage gs runs pass gs / NST % 2 of conv gs / (2 NST); both passes stream the
+    // conv's weight stages
+    if constexpr (P == 2) s = (s / (2 * G::NST)) * G::NST + s % G::NST;
 #pragma unroll
     for (int k = 0; k < G::KS; ++k)
         ring_issue_k<F, PTN, NB, P, WG, SLOT>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * G::ROWB,
@@ -389,14 +406,14 @@ __device__ __forceinline__ int tap_offset(const TapAddr& t, int kc) {
 // One 3x3 'same' conv over the NB LDS images at X (board b at X + b*ACT_BYTES):
 // acc[ct][t] = W * X (fp32 accumulate), tile t = b*PT + pt.  gs0 = global stage index of this
 // conv's first stage; on entry stages gs0 .. gs0+R-2 are in flight in ring slots 0..R-2.
-template <int F, int PTN, int NB, int P, int WG, int ST>
+template <int F, int PTN, int NB, int P, int WG, int PASS, int ST>
 __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                            f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                            bf16x8 (&b)[2][Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
                                            const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane,
                                            const Board& bd) {
     using G = Geo<F, PTN, NB, P, WG>;
-    constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC, P2 = G::P2;
+    constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC, P2 = G::P2, WP = G::WP;
     // refill the slot stage ST-1 consumed with stage ST+R-1, then wait for stage ST
     ring_issue<F, PTN, NB, P, WG, (ST + R - 1) % R>(ring, wres, woff, gs0 + ST + R - 1, gmax);
     if constexpr (!G::TRACKED) {
@@ -428,13 +445,16 @@ __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, P
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
-                const bf16x8 w_hi = ring.r[ST % R][k][ct * P2];
+                const bf16x8 w_hi = ring.r[ST % R][k][ct * WP];
                 acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[j & 1][t][0], acc[ct][t], 0, 0, 0);
-                if constexpr (P2 == 2) {   // split precision: + hi*lo + lo*hi
-                    const bf16x8 w_lo = ring.r[ST % R][k][ct * P2 + 1];
+                if constexpr (P == 3) {   // split precision: + hi*lo + lo*hi
+                    const bf16x8 w_lo = ring.r[ST % R][k][ct * WP + 1];
                     acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[j & 1][t][1], acc[ct][t], 0, 0, 0);
                     acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[j & 1][t][0], acc[ct][t], 0, 0, 0);
-                }
+                } else if constexpr (P == 2 && PASS == 0) {   // two-pass split, hi image: + lo*hi
+                    const bf16x8 w_lo = ring.r[ST % R][k][ct * WP + 1];
+                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[j & 1][t][0], acc[ct][t], 0, 0, 0);
+                }   // (P = 2, pass 1: the lo image, hi*lo only)
             }
         // interleave the next k-step's B reads with this k-step's MFMAs (CT MFMAs, one ds_read,
         // ...) instead of the compiler's cluster of reads ahead of the MFMA run: measured 2-4 %
@@ -460,26 +480,29 @@ __device__ __forceinline__ void ring_prime(Ring<F, PTN, NB, P, WG>& ring, const 
     (ring_issue<F, PTN, NB, P, WG, S>(ring, wres, woff, S, gmax), ...);
 }
 
-template <int F, int PTN, int NB, int P, int WG, int... ST>
+template <int F, int PTN, int NB, int P, int WG, int PASS, int... ST>
 __device__ __forceinline__ void conv_stages(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                             f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                             bf16x8 (&b)[2][Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
                                             const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane,
                                             const Board& bd, std::integer_sequence<int, ST...>) {
-    (conv_stage<F, PTN, NB, P, WG, ST>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd), ...);
+    (conv_stage<F, PTN, NB, P, WG, PASS, ST>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd), ...);
 }
 
-template <int F, int PTN, int NB, int P, int WG = 1>
+// PASS (P = 2): 0 starts the accumulators, 1 adds to them
+template <int F, int PTN, int NB, int P, int WG = 1, int PASS = 0>
 __device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                         f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                         const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane,
                                         const Board& bd) {
     using G = Geo<F, PTN, NB, P, WG>;
     constexpr int PT = G::PT, TT = G::TT;
+    if constexpr (PASS == 0) {
 #pragma unroll
-    for (int ct = 0; ct < G::CT; ++ct)
+        for (int ct = 0; ct < G::CT; ++ct)
 #pragma unroll
-        for (int t = 0; t < TT; ++t) acc[ct][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int t = 0; t < TT; ++t) acc[ct][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     bf16x8 b[2][TT][G::P2];
     // k-step 0 = tap 0 (dy = dx = -1), kc 0
     launder(lane);
@@ -491,8 +514,8 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN,
 #pragma unroll
             for (int h = 0; h < G::P2; ++h) b[0][bb * PT + pt][h] = *(const bf16x8*)(a + bb * G::ACT_BYTES + h * G::HALF);
     }
-    conv_stages<F, PTN, NB, P, WG>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd,
-                               std::make_integer_sequence<int, G::NST>{});
+    conv_stages<F, PTN, NB, P, WG, PASS>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd,
+                                     std::make_integer_sequence<int, G::NST>{});
 }
 
 // ---- looped conv: one iteration = U ring stages = TPI taps; tap0 = the iteration's first tap ----
@@ -507,7 +530,8 @@ __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F,
                                              const __bf16* wres, uint32_t woff, int gs_it, int gmax, int& lane,
                                              const Board& bd, int tap0, bool last_it) {
     using G = Geo<F, PTN, NB, P, WG>;
-    constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, KC = G::KC, P2 = G::P2;
+    constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, KC = G::KC, P2 = G::P2, WP = G::WP;
+    static_assert(P != 2, "two-pass split precision runs the single-image conv");
     static_assert(G::U % R == 0, "ring slots must be static within an iteration");
     ring_issue<F, PTN, NB, P, WG, (ST + R - 1) % R>(ring, wres, woff, gs_it + ST + R - 1, gmax);
     if constexpr (!G::TRACKED) {
@@ -532,10 +556,10 @@ __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F,
                 const int t = bb * PT + pt;
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct) {
-                    const bf16x8 w_hi = ring.r[ST % R][k][ct * P2];
+                    const bf16x8 w_hi = ring.r[ST % R][k][ct * WP];
                     acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][0], acc[ct][t], 0, 0, 0);
                     if constexpr (P2 == 2) {
-                        const bf16x8 w_lo = ring.r[ST % R][k][ct * P2 + 1];
+                        const bf16x8 w_lo = ring.r[ST % R][k][ct * WP + 1];
                         acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][1], acc[ct][t], 0, 0, 0);
                         acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[t][0], acc[ct][t], 0, 0, 0);
                     }
@@ -673,15 +697,44 @@ __device__ __forceinline__ f32x4 pre_act(f32x4 v, const float4& sc, const float4
     return v;
 }
 
+// P = 2, after an epilogue wrote the lo parts of the image (and a barrier): copy them to the
+// workgroup's lo scratch in device memory, then write the hi parts of acc into the image.
+// LD = true: the other direction (the lo scratch into the image, for a conv's second pass).
+template <int F, int PTN, bool LD>
+__device__ __forceinline__ void lo_copy(char* X, char* xlo, int npos, int tid) {
+    using G = Geo<F, PTN, 1, 2>;
+    const int n16 = npos * G::ROWS / 16;   // the on-board rows (the zero and scratch rows stay)
+    uint4* img = (uint4*)X;
+    uint4* glo = (uint4*)xlo;
+#pragma unroll 4
+    for (int i = tid; i < n16; i += 256) {
+        if constexpr (LD) img[i] = glo[i];
+        else glo[i] = img[i];
+    }
+}
+template <int F, int PTN>
+__device__ __forceinline__ void save_lo_write_hi(char* X, char* xlo, const f32x4 (&acc)[Geo<F, PTN, 1, 2>::CT][Geo<F, PTN, 1, 2>::TT],
+                                                 int npos, int tid, int co_base, int li, int g) {
+    using G = Geo<F, PTN, 1, 2>;
+    lo_copy<F, PTN, false>(X, xlo, npos, tid);
+    __syncthreads();
+#pragma unroll
+    for (int ct = 0; ct < G::CT; ++ct)
+#pragma unroll
+        for (int t = 0; t < G::TT; ++t) store_act<F, PTN, 1, false>(X, 16 * t + li, co_base + 16 * ct + 4 * g, acc[ct][t], npos);
+    __syncthreads();
+}
+
 // The trunk of NB boards per workgroup of 4 waves (trunk_kernel / trunk_kernel_v2 below).  V2:
 // pre-activation blocks with optional squeeze-excite (a separate instantiation, so the v1 kernels'
 // register allocation is not burdened by the v2 epilogues).
 template <int F, int PTN, int NB, int WPE, int P, bool V2, int WG = 1>
 __device__ __forceinline__ void trunk_body(const KParams& kp) {
     using G = Geo<F, PTN, NB, P, WG>;
-    static_assert(P == 1 || (P == 3 && (NB == 1 || G::WRAP) && (G::CT <= 2 || G::SI)),
+    static_assert(P == 1 || (P == 3 && (NB == 1 || G::WRAP) && (G::CT <= 2 || G::SI)) || (P == 2 && G::SI && !V2),
                   "split precision: F <= 128 (F = 256: single image)");
     constexpr int P2 = G::P2;
+    constexpr int IP2 = G::WP;    // bf16 parts of the initial conv's operands (im2col scratch, w0 / w0lo)
     constexpr int PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, kThreads = 256;
     const int NPOS = kp.npos, H = kp.H, W = kp.W;     // the board (NPOS <= G::NPOS)
     Board bd{H, W, NPOS, kp.wmagic, {}};
@@ -748,7 +801,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
 
     // prime the weight ring: stages 0 .. R-2 of the trunk stream
     const uint32_t woff = (uint32_t)((co_base + li) * G::ROWB + 16 * g);   // lane's fragment bytes within a k-step
-    const int gmax = 2 * kp.B * G::NST - 1;
+    const int gmax = (P == 2 ? 4 : 2) * kp.B * G::NST - 1;   // P = 2: two passes per conv
     Ring<F, PTN, NB, P, WG> ring;
     if (kp.B > 0) ring_prime<F, PTN, NB, P, WG>(ring, kp.wres, woff, gmax, std::make_integer_sequence<int, R - 1>{});
 
@@ -756,6 +809,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     f32x4 resid[RG ? 1 : CT][RG ? 1 : TT];
     // global residual of this wave: tile (ct, t) at rg[(ct * TT + t) * 64]
     f32x4* rg = RG ? kp.resid + ((size_t)(blockIdx.x * 4 + wave) * CT * TT) * 64 + lane : nullptr;
+    // P = 2: this workgroup's lo image, after the grid's residual scratch
+    char* xlo = P == 2 ? (char*)kp.resid + (size_t)gridDim.x * G::RESID_BYTES + (size_t)blockIdx.x * G::LO_BYTES : nullptr;
 
     for (int i = threadIdx.x; i < 2 * kp.B * F; i += kThreads * WG) btab[i] = kp.bres[i];
     for (int i = tid; i < NB * G::ZROWS * G::ROWS / 4; i += kThreads) {
@@ -782,7 +837,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         __syncthreads();
         // IM[p][k], k = tap*C + c (a 1x1 initial conv: k = c), zero padded to K0: zero the image,
         // then one thread per (position, tap) copies its C channels (compile-time divisors only)
-        for (int i = tid; i < P2 * align16((NPOS + 1) * imrow) / 16; i += kThreads) ((uint4*)IM)[i] = uint4{0u, 0u, 0u, 0u};
+        for (int i = tid; i < IP2 * align16((NPOS + 1) * imrow) / 16; i += kThreads) ((uint4*)IM)[i] = uint4{0u, 0u, 0u, 0u};
         __syncthreads();
         const int T0 = kp.k0taps;
         for (int i = tid; i < NPOS * T0; i += kThreads) {
@@ -798,7 +853,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                     const int o = p * imrow + ((((k >> 3) ^ (p & imswz))) << 4) + (k & 7) * 2;
                     const float v = src[c * NPOS];
                     *(__bf16*)(IM + o) = (__bf16)v;
-                    if constexpr (P2 == 2) *(__bf16*)(IMlo + o) = (__bf16)bf16_lo(v);
+                    if constexpr (IP2 == 2) *(__bf16*)(IMlo + o) = (__bf16)bf16_lo(v);
                 }
             }
         }
@@ -817,7 +872,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
             for (int ct = 0; ct < CT; ++ct) {
                 const size_t o = ((size_t)(s * F + co_base + 16 * ct + li)) * 32 + 8 * g;
                 x[ct] = *(const bf16x8*)(kp.w0 + o);
-                if constexpr (P2 == 2) xl[ct] = *(const bf16x8*)(kp.w0lo + o);
+                if constexpr (IP2 == 2) xl[ct] = *(const bf16x8*)(kp.w0lo + o);
             }
         };
         load_w0(0, a, alo);
@@ -834,7 +889,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                 for (int ct = 0; ct < CT; ++ct) {
                     f32x4& c = acc[ct][bb * PT + pt];
                     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], bq, c, 0, 0, 0);
-                    if constexpr (P2 == 2) {
+                    if constexpr (IP2 == 2) {
                         const bf16x8 bql = *(const bf16x8*)(IMlo + o);
                         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], bql, c, 0, 0, 0);
                         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[ct], bq, c, 0, 0, 0);
@@ -845,7 +900,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct) {
                     a[ct] = an[ct];
-                    if constexpr (P2 == 2) alo[ct] = alon[ct];
+                    if constexpr (IP2 == 2) alo[ct] = alon[ct];
                 }
             }
         }
@@ -878,6 +933,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
             }
         }
         __syncthreads();    // scratch is reused by the next board
+        if constexpr (P == 2) save_lo_write_hi<F, PTN>(X0, xlo, acc, NPOS, tid, co_base, li, g);
     }
     for (int i = tid; i < NB * G::ZROWS * G::ROWS / 4; i += kThreads) {
         const int bb = i / (G::ZROWS * G::ROWS / 4), j = i % (G::ZROWS * G::ROWS / 4);
@@ -892,7 +948,15 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         for (int cv = 0; cv < 2 * kp.B; ++cv) {
             const bool second = cv & 1;
             const float* bt = btab + cv * F;
-            conv3x3<F, PTN, NB, P, WG>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane, bd);
+            if constexpr (P == 2) {
+                conv3x3<F, PTN, NB, P, WG, 0>(X0, ring, acc, kp.wres, woff, (2 * cv) * G::NST, gmax, lane, bd);
+                __syncthreads();    // every wave has finished reading the hi image
+                lo_copy<F, PTN, true>(X0, xlo, NPOS, tid);   // the lo image
+                __syncthreads();
+                conv3x3<F, PTN, NB, P, WG, 1>(X0, ring, acc, kp.wres, woff, (2 * cv + 1) * G::NST, gmax, lane, bd);
+            } else {
+                conv3x3<F, PTN, NB, P, WG>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane, bd);
+            }
             __syncthreads();    // every wave has finished reading the image it is about to overwrite
             // residual tile addresses are formed here, not hoisted out of the loop (44 x 64-bit)
             f32x4* rgc = rg;
@@ -953,12 +1017,13 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                     if (second) {
                         if constexpr (RG) rgc[(ct * TT + t) * 64] = v;
                         else resid[ct][t] = v;
-                        acc[ct][t] = v;
                     }
+                    if (second || P == 2) acc[ct][t] = v;
                     store_act<F, PTN, P, !G::SI>(X0, 16 * t + li, co, v, NPOS);
                 }
             }
             __syncthreads();
+            if constexpr (P == 2) save_lo_write_hi<F, PTN>(X0, xlo, acc, NPOS, tid, co_base, li, g);
         }
     } else
     for (int blk = 0; blk < kp.B; ++blk) {

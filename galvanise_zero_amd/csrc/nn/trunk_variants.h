@@ -34,7 +34,7 @@ KernelChoice kernel_for() {
     k.act_bytes = Geo<F, PTN, NB, P>::ACT_BYTES;
     k.nb = NB;
     k.single_image = Geo<F, PTN, NB, P>::SI;
-    k.resid_bytes = Geo<F, PTN, NB, P>::RESID_BYTES;
+    k.resid_bytes = Geo<F, PTN, NB, P>::RESID_BYTES + Geo<F, PTN, NB, P>::LO_BYTES;
     std::snprintf(k.name, sizeof(k.name), "gznn::trunk_kernel%s<%d, %d, %d, %d, %d>", V2 ? "_v2" : "", F, PTN, NB, WPE, P);
     return k;
 }
@@ -57,11 +57,15 @@ template <int F, int PTN, bool V2 = false>
 KernelChoice variants(int v, int precision) {
     if (precision == 3) {
         // F = 256 split: one board per workgroup in a single image of hi + lo wrapped rows, where
-        // that image and the bias table fit the LDS (10 x 10; a 13 x 13 image needs 182 KB)
+        // that image and the bias table fit the LDS (10 x 10); otherwise (13 x 13: the hi + lo
+        // image needs 189 KB) the two-pass kernel (P = 2: one part in the LDS at a time)
         if constexpr (F == 256) {
             if constexpr (Geo<F, PTN, 1, 3>::SI && Geo<F, PTN, 1, 3>::ACT_BYTES + 40 * 1024 <= 160 * 1024 &&
-                          !Geo<F, PTN, 1, 3>::RG)
+                          !Geo<F, PTN, 1, 3>::RG) {
                 if (v == 11) return kernel_for<F, PTN, 1, 1, 3, V2>();
+            } else if constexpr (!V2 && Geo<F, PTN, 1, 2>::SI && Geo<F, PTN, 1, 2>::ACT_BYTES + 16 * 1024 <= 160 * 1024) {
+                if (v == 11) return kernel_for<F, PTN, 1, 1, 2, V2>();
+            }
             return KernelChoice{};
         }
         if constexpr (F <= 128 && PTN <= 4) {

@@ -146,7 +146,9 @@ TOL_FP32 = (2e-4, 5e-5)          # max |err|, mean |err|
 TOL_FP32_KL = 5e-7               # max over rows of KL(oracle || kernel)
 SPLIT = ["cfg1", "cfg2", "cfg3", "b0_8x8", "leaky_v3_8x8", "nchw_6x6", "legacy_v1_8x8", "x6_102_json",
          # F = 256 on 10 x 10 (single-image split kernel): amazons cfg5 and a leaky / draw-head net
-         "cfg5", "b0_10x10_f256_v3"]
+         "cfg5", "b0_10x10_f256_v3",
+         # F = 256 on 13 x 13 (two-pass split kernel, P = 2): hexLG13 cfg4 and a 2-block net
+         "cfg4", "b2_13x13_f256"]
 
 
 def _net_p(desc, seed, device, name, precision):
@@ -195,7 +197,7 @@ def test_fp32_tolerance_detects_one_bf16_ulp(hip_device):
     assert max(errs) > TOL_FP32[0]
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
 def test_batch_invariance_fp32(name, hip_device):
     desc = VARIANTS[name]
     net, _ = _net_p(desc, 3, hip_device, name, "fp32")
