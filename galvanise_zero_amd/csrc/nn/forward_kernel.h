@@ -345,16 +345,24 @@ template <int WP, int ROWB, int FR>
 struct FragOff {
     static constexpr int value = (FR / WP) * 16 * ROWB + (FR % WP) * 64;
 };
-template <int F, int PTN, int NB, int P, int WG, int SLOT, int... FRS>
+template <int F, int PTN, int NB, int P, int WG, int SLOT, bool HI_ONLY, int FR>
+__device__ __forceinline__ void ring_issue_f(Ring<F, PTN, NB, P, WG>& ring, int k, uint32_t woff, const char* sb) {
+    using G = Geo<F, PTN, NB, P, WG>;
+    if constexpr (!HI_ONLY || FR % G::WP == 0) {
+        if constexpr (G::TRACKED)
+            ring.r[SLOT][k][FR] = *(const bf16x8*)(sb + woff + FragOff<G::WP, G::ROWB, FR>::value);
+        else
+            ring.r[SLOT][k][FR] = gload_issue<FragOff<G::WP, G::ROWB, FR>::value>(woff, sb);
+    }
+}
+template <int F, int PTN, int NB, int P, int WG, int SLOT, bool HI_ONLY, int... FRS>
 __device__ __forceinline__ void ring_issue_k(Ring<F, PTN, NB, P, WG>& ring, int k, uint32_t woff, const char* sb,
                                              std::integer_sequence<int, FRS...>) {
-    using G = Geo<F, PTN, NB, P, WG>;
-    if constexpr (G::TRACKED)
-        ((ring.r[SLOT][k][FRS] = *(const bf16x8*)(sb + woff + FragOff<G::WP, G::ROWB, FRS>::value)), ...);
-    else
-        ((ring.r[SLOT][k][FRS] = gload_issue<FragOff<G::WP, G::ROWB, FRS>::value>(woff, sb)), ...);
+    (ring_issue_f<F, PTN, NB, P, WG, SLOT, HI_ONLY, FRS>(ring, k, woff, sb), ...);
 }
-template <int F, int PTN, int NB, int P, int WG, int SLOT>
+// HI_ONLY (P = 2, a stage of a conv's second pass, which multiplies by the hi parts only): the lo
+// fragments are not loaded (their slot registers are not read in that pass; TRACKED kernels only)
+template <int F, int PTN, int NB, int P, int WG, int SLOT, bool HI_ONLY = false>
 __device__ __forceinline__ void ring_issue(Ring<F, PTN, NB, P, WG>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
     using G = Geo<F, PTN, NB, P, WG>;
     int s = gs < gmax ? gs : gmax;
@@ -363,8 +371,8 @@ __device__ __forceinline__ void ring_issue(Ring<F, PTN, NB, P, WG>& ring, const 
     if constexpr (P == 2) s = (s / (2 * G::NST)) * G::NST + s % G::NST;
 #pragma unroll
     for (int k = 0; k < G::KS; ++k)
-        ring_issue_k<F, PTN, NB, P, WG, SLOT>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * G::ROWB,
-                                           std::make_integer_sequence<int, G::NFR>{});
+        ring_issue_k<F, PTN, NB, P, WG, SLOT, HI_ONLY>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * G::ROWB,
+                                                    std::make_integer_sequence<int, G::NFR>{});
 }
 
 // LDS byte offset (within a board image) of a lane's B fragment for tap `tap`, position tile pt,
@@ -415,7 +423,11 @@ __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, P
     using G = Geo<F, PTN, NB, P, WG>;
     constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, TT = G::TT, KC = G::KC, P2 = G::P2, WP = G::WP;
     // refill the slot stage ST-1 consumed with stage ST+R-1, then wait for stage ST
-    ring_issue<F, PTN, NB, P, WG, (ST + R - 1) % R>(ring, wres, woff, gs0 + ST + R - 1, gmax);
+    // P = 2: the stage issued here belongs to this pass, or (past the pass's last stage) to the
+    // next one; the second pass's stages need the hi parts only
+    constexpr bool next_in_pass = ST + R - 1 < G::NST;
+    constexpr bool hi_only = P == 2 && G::TRACKED && (next_in_pass ? PASS == 1 : PASS == 0);
+    ring_issue<F, PTN, NB, P, WG, (ST + R - 1) % R, hi_only>(ring, wres, woff, gs0 + ST + R - 1, gmax);
     if constexpr (!G::TRACKED) {
         ring_wait<(R - 1) * G::LPS>();
 #pragma unroll

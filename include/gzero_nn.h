@@ -43,7 +43,8 @@ typedef struct gz_net_desc {
      *   GZ_PRECISION_BF16 (0 or 1): bf16 operands, fp32 accumulation and residual stream;
      *   GZ_PRECISION_SPLIT (3): fp32 accuracy -- each fp32 operand as bf16 hi + bf16 lo and each
      *   product as hi*hi + hi*lo + lo*hi on the MFMA (~16 significant bits per operand, fp32
-     *   accumulation); F <= 128.  The heads are fp32 in both modes. */
+     *   accumulation); F <= 128 on boards <= 64 positions, F = 256 on boards <= 13 x 13 (single
+     *   image; 13 x 13 by two passes per conv).  The heads are fp32 in both modes. */
     int precision;
     /* v2 (pre-activation) trunk, model.py:78-151 (the reference's features=True templates and its
      * non-legacy model files); all zero = v1. */
