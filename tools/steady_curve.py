@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--spin-yield", type=int, default=1000)
     ap.add_argument("--out", default="")
+    ap.add_argument("--roll-seconds", type=float, default=0,
+                    help="clear the unique-states filters every S seconds, as the reference worker does "
+                         "at each new generation (worker.py:160); 0 = never")
     args = ap.parse_args()
     import bench
     from galvanise_zero_amd._native import HipNet
@@ -40,7 +43,7 @@ def main():
     from galvanise_zero_amd.runner import SelfPlayRunner
     sm, t, desc = bench.setup_game(args.config)
     # the bench's network: bf16x3 split where compiled, the bench's weights
-    net = HipNet(desc, 0, "fp32" if desc.cnn_filter_size <= 128 or desc.hw <= 112 else "bf16")
+    net = HipNet(desc, 0, "fp32")
     net.set_weights(to_blob(random_weights(desc, 7921)))
     threads = args.threads or max(1, bench.cpu_share())   # as bench.py (cgroup quota aware)
     conf = bench.selfplay_conf("template", BASELINE_CONFIGS[args.config]["evals"])
@@ -52,8 +55,14 @@ def main():
     t0 = time.time()
     prev, tp = r.stats(), t0
     rows_log = []
+    next_roll = args.roll_seconds if args.roll_seconds > 0 else float("inf")
+    rolls = 0
     while time.time() - t0 < args.seconds:
         time.sleep(args.interval)
+        if time.time() - t0 >= next_roll:
+            r.clear_unique_states()
+            rolls += 1
+            next_roll += args.roll_seconds
         st, now = r.stats(), time.time()
         dt = now - tp
         d = {k: st[k] - prev[k] for k in st}
@@ -63,6 +72,7 @@ def main():
                "rows_per_launch": d["rows"] / max(1, d["kernel_launches"]),
                "nn_free_playouts_per_leaf": (d["tree_playouts"] - d["rows"]) / max(1, d["rows"]),
                "engine_idle": d["engine_idle_ms"] / 1e3 / dt / threads,
+               "samples_per_s": d["samples"] / dt, "dupes_per_s": d["dupes"] / dt, "rolls": rolls,
                "rss_gb": rss_gb(),
                "evals_per_game_cum": st["completed_game_evals"] / max(1, st["games_completed"])}
         rows_log.append(row)
