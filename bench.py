@@ -56,6 +56,39 @@ TRAFFIC_SOURCE = {
                                            "separate passes, 1024-row launches; FETCH x2 gfx950 correction, 1 KB units)"}
 
 
+PEAK_HBM_GBPS = 8000.0         # MI355X HBM3E (MI355X_MICROARCH.md)
+# SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE (summed over the 8 XCDs) per launch of the dominant
+# kernel at 1,024 rows, from one rocprofv3 --pmc pass (tools/gpu_pmc_r04.sh)
+PMC_PER_LAUNCH = {}
+
+
+def per_game_cost(o, threads):
+    """Per-game cost by the game's ordinal within its slot (gz_ordinal_stats of rank 0's runner, the
+    whole run): is a slot's k-th game dearer than its first?  Plus the renewal-reward estimate of the
+    stationary rate: leaf evaluations per engine-second over the completed games, times the engine
+    threads (a lower bound's complement: long games still in flight are under-represented)."""
+    rows = []
+    for k in range(len(o["games"])):
+        g = o["games"][k]
+        if g == 0:
+            continue
+        rows.append({"ordinal": k + 1 if k + 1 < len(o["games"]) else "%d+" % (k + 1), "games": g,
+                     "evals_per_game": o["evals"][k] / g,
+                     "nn_free_playouts_per_game": (o["tree_playouts"][k] - o["evals"][k]) / g,
+                     "moves_per_game": o["moves"][k] / g, "spin_epochs_per_game": o["spin_epochs"][k] / g,
+                     "engine_ms_per_game": 1e3 * o["engine_s"][k] / g,
+                     "evals_per_engine_s": o["evals"][k] / o["engine_s"][k] if o["engine_s"][k] > 0 else None})
+    ev, es = sum(o["evals"]), sum(o["engine_s"])
+    hist = {"<%d ms" % (1 << k): c for k, c in enumerate(o["cost_hist"]) if c}
+    return {"by_ordinal": rows, "engine_ms_histogram": hist,
+            "completed_games_evals_per_engine_s": ev / es if es > 0 else None,
+            "stationary_estimate_leaf_evals_per_s": threads * ev / es if es > 0 else None,
+            "in_flight": {"games": o["inflight_games"], "engine_s": o["inflight_engine_s"],
+                          "evals": o["inflight_evals"],
+                          "evals_per_engine_s": o["inflight_evals"] / o["inflight_engine_s"]
+                          if o["inflight_engine_s"] > 0 else None}}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -352,6 +385,7 @@ def main():
     runner.wait_rows(s0["rows"] + args.steps * args.step_rows, timeout_s=3600, progress=heartbeat)
     s1 = runner.stats()
     t1 = time.perf_counter()
+    ordinals = runner.ordinal_stats()
     barrier()
     runner.stop()
     elapsed = t1 - t0
@@ -504,6 +538,16 @@ def main():
         }
         if dom:
             out["roofline"]["l2_weight_stream"] = per_variant[dom]["l2_weight_stream"]
+            pmc = PMC_PER_LAUNCH.get(dom) if args.config == 2 else None
+            if pmc:
+                # counter figures of the same kernel from its committed PMC run (PMC counters cannot be
+                # read inside the timed run): MFMA pipe busy / (SIMDs x active cycles), and fabric bytes
+                # per launch over this window's average launch time against the 8 TB/s HBM peak
+                busy = pmc["mfma_busy_cycles"] / (pmc["grbm_gui_active"] / 8 * NUM_CUS * 4)
+                gbps = out["roofline"]["traffic"] / (per_variant[dom]["avg_kernel_ms"] / 1e3) / 1e9
+                out["roofline"].update({"mfma_busy_frac": busy, "hbm_GBps": gbps, "hbm_peak_GBps": PEAK_HBM_GBPS,
+                                        "hbm_frac": gbps / PEAK_HBM_GBPS, "pmc_source": pmc["source"]})
+        out["per_game_cost"] = per_game_cost(ordinals, threads)
     runner.close()   # frees the games' trees before the CPU baseline
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:

@@ -303,6 +303,33 @@ class GzPoolStats(ctypes.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+GZ_ORDINALS, GZ_COST_HIST = 8, 32
+
+
+class GzOrdinalStats(ctypes.Structure):
+    """gz_ordinal_stats (include/gzero_engine.h): per-game cost by the game's ordinal in its slot."""
+    _fields_ = [(n, ctypes.c_long * GZ_ORDINALS) for n in ("games", "evals", "tree_playouts", "moves", "spin_epochs")] + \
+               [("engine_s", ctypes.c_double * GZ_ORDINALS), ("cost_hist", ctypes.c_long * GZ_COST_HIST),
+                ("inflight_games", ctypes.c_long), ("inflight_engine_s", ctypes.c_double),
+                ("inflight_evals", ctypes.c_long)]
+
+    def as_dict(self):
+        out = {}
+        for n, _ in self._fields_:
+            v = getattr(self, n)
+            out[n] = list(v) if hasattr(v, "__len__") else v
+        return out
+
+
+def set_verify_fastpath(on):
+    """Run-time GZ_VERIFY_FASTPATH (process-wide); returns the previous setting."""
+    return bool(engine_lib().gz_engine_set_verify_fastpath(1 if on else 0))
+
+
+def verified_decisions():
+    return int(engine_lib().gz_engine_verified_decisions())
+
+
 _VP = ctypes.c_void_p
 _U64P = ctypes.POINTER(ctypes.c_uint64)
 _IP = ctypes.POINTER(ctypes.c_int)
@@ -365,6 +392,9 @@ _ENGINE_SIGS = {
     "gz_pool_fetch_samples": (_VP, [_VP]),
     "gz_pool_fetch_samples_n": (_VP, [_VP, ctypes.POINTER(ctypes.c_long)]),
     "gz_pool_take_sample_count": (ctypes.c_long, [_VP]),
+    "gz_pool_add_ordinal_stats": (ctypes.c_int, [_VP, _VP]),
+    "gz_engine_set_verify_fastpath": (ctypes.c_int, [ctypes.c_int]),
+    "gz_engine_verified_decisions": (ctypes.c_long, []),
 }
 
 
@@ -477,5 +507,6 @@ def runner_lib():
         lib.gz_runner_update_network.argtypes = [_VP, _VP, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_double]
         lib.gz_runner_roll_info.argtypes = [_VP, ctypes.POINTER(ctypes.c_long), ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_long)]
+        lib.gz_runner_ordinal_stats.argtypes = [_VP, ctypes.POINTER(GzOrdinalStats)]
         lib._gz_runner_typed = True
     return lib

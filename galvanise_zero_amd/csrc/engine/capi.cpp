@@ -280,6 +280,7 @@ extern "C" void gz_supervisor_destroy(gz_supervisor* s) {
     if (s) {
         delete s->impl;
         delete s;
+        node_cache_flush();
     }
 }
 extern "C" int gz_supervisor_start_self_play(gz_supervisor* s, int num_workers, const gz_selfplay_config* conf) {
@@ -347,6 +348,7 @@ extern "C" void gz_player_destroy(gz_player* p) {
     if (p) {
         delete p->impl;
         delete p;
+        node_cache_flush();
     }
 }
 extern "C" int gz_player_reset(gz_player* p, int game_depth) {
@@ -461,6 +463,7 @@ extern "C" void gz_pool_destroy(gz_pool* p) {
         delete p->impl;
         delete p->own_unique;
         delete p;
+        node_cache_flush();   // the trees were freed onto this thread's lists
     }
 }
 extern "C" int gz_pool_start(gz_pool* p, const gz_selfplay_config* conf) {
@@ -504,6 +507,34 @@ extern "C" char* gz_pool_fetch_samples_n(gz_pool* p, long* count) {
     s.clear();
     return dup_string(j);
 }
+static_assert(GZ_ORDINALS == OrdinalStats::kOrdinals && GZ_COST_HIST == OrdinalStats::kHist, "ordinal stats layout");
+extern "C" int gz_pool_add_ordinal_stats(gz_pool* p, gz_ordinal_stats* out) {
+    if (!p || !out) return fail("null argument");
+    const OrdinalStats& o = p->impl->getStats().ord;
+    const double hz = tsc_hz();
+    for (int k = 0; k < GZ_ORDINALS; ++k) {
+        out->games[k] += o.games[k];
+        out->evals[k] += o.evals[k];
+        out->tree_playouts[k] += o.tree_playouts[k];
+        out->moves[k] += o.moves[k];
+        out->spin_epochs[k] += o.spin_epochs[k];
+        out->engine_s[k] += (double)o.cycles[k] / hz;
+    }
+    for (int k = 0; k < GZ_COST_HIST; ++k) out->cost_hist[k] += o.cost_hist[k];
+    long g = 0, e = 0;
+    double s = 0;
+    p->impl->inflight(&g, &s, &e);
+    out->inflight_games += g;
+    out->inflight_engine_s += s;
+    out->inflight_evals += e;
+    return 0;
+}
+extern "C" int gz_engine_set_verify_fastpath(int on) {
+    const bool prev = get_verify_fastpath();
+    set_verify_fastpath(on != 0);
+    return prev ? 1 : 0;
+}
+extern "C" long gz_engine_verified_decisions(void) { return verified_decisions(); }
 extern "C" long gz_pool_take_sample_count(gz_pool* p) {
     std::vector<Sample*>& s = p->impl->getSamples();
     const long n = (long)s.size();

@@ -3,9 +3,13 @@
 #include <sys/mman.h>
 #include <unistd.h>
 
+#include <x86intrin.h>
+
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <thread>
 
 // gz_ctx_switch(void** save_sp, void* load_sp): SysV x86-64.  Saves callee-saved GPRs, mxcsr and
 // the x87 control word on the current stack, stores rsp into *save_sp, loads load_sp and restores
@@ -72,6 +76,9 @@ extern "C" void gz_coro_entry(Coro* c) {
         std::abort();
     }
     t_current = p;
+    const uint64_t now = __rdtsc();
+    c->cycles += now - c->resumed_at;
+    p->resumed_at = now;
     void* dummy;
     gz_ctx_switch(&dummy, p->sp);
     std::abort();   // never resumed
@@ -118,8 +125,28 @@ void coro_switch_to(Coro* to) {
     Coro* from = coro_current();
     if (from == to) return;
     t_current = to;
+    const uint64_t now = __rdtsc();
+    from->cycles += now - from->resumed_at;
+    to->resumed_at = now;
     gz_ctx_switch(&from->sp, to->sp);
     // resumed: t_current was set by whoever switched to us
+}
+
+uint64_t coro_cycles_now() {
+    const Coro* c = coro_current();
+    return c->cycles + (__rdtsc() - c->resumed_at);
+}
+
+double tsc_hz() {
+    static const double hz = [] {
+        const auto t0 = std::chrono::steady_clock::now();
+        const uint64_t c0 = __rdtsc();
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        const uint64_t c1 = __rdtsc();
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return (double)(c1 - c0) / s;
+    }();
+    return hz;
 }
 
 void coro_destroy(Coro* c) {

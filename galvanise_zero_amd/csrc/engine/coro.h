@@ -11,6 +11,7 @@
 #pragma once
 
 #include <cstddef>
+#include <cstdint>
 #include <functional>
 
 namespace gz {
@@ -22,6 +23,10 @@ struct Coro {
     Coro* parent = nullptr;        // receives control when the body returns
     std::function<void()> body;
     bool dead = false;
+    // TSC cycles this coroutine has run (updated when it is switched away from), and the TSC
+    // value when it was last switched to: per-game engine time (selfplay.cpp) at one rdtsc a switch
+    uint64_t cycles = 0;
+    uint64_t resumed_at = 0;
 };
 
 // The coroutine currently running on this thread (a per-thread root Coro when none).
@@ -32,6 +37,12 @@ Coro* coro_create(std::function<void()> body, Coro* parent, size_t stack_size = 
 
 // Switch from the current coroutine to `to`.  Returns when something switches back.
 void coro_switch_to(Coro* to);
+
+// TSC cycles the current coroutine has run so far, including its current stretch.
+uint64_t coro_cycles_now();
+
+// TSC ticks per second (calibrated once against the steady clock, ~20 ms on first call).
+double tsc_hz();
 
 // Free a coroutine (must not be running).  Dead coroutines may be destroyed by anyone.
 void coro_destroy(Coro* c);

@@ -335,12 +335,36 @@ void PuctEvaluator::balanceFirstMoves(int max_moves) {
 // the identical child.  Otherwise the literal sorted path runs.  tests/test_puct_parity.py checks
 // the engine against the oracle (which always sorts); GZ_VERIFY_FASTPATH=1 cross-checks at run time.
 
-static bool verify_fastpath() {
-    static const bool v = [] {
-        const char* e = std::getenv("GZ_VERIFY_FASTPATH");
-        return e != nullptr && e[0] == '1';
-    }();
-    return v;
+// Process-wide switch: GZ_VERIFY_FASTPATH=1 at load, or gz_engine_set_verify_fastpath() at any
+// time (a live runner can age unverified, then verify a later window).  Each fast path reads it
+// once per decision, so a flip takes effect at the next selection / spin run.
+static std::atomic<bool> g_verify_fastpath{[] {
+    const char* e = std::getenv("GZ_VERIFY_FASTPATH");
+    return e != nullptr && e[0] == '1';
+}()};
+// Fast-path decisions re-checked by the verification (diagnostics: a test shows the verified window
+// really ran verified): one padded counter per thread slot, summed on read.
+namespace {
+struct alignas(64) VerifySlot {
+    std::atomic<long> n{0};
+};
+constexpr int kVerifySlots = 256;
+VerifySlot g_verified[kVerifySlots];
+std::atomic<int> g_verify_next_slot{0};
+struct VerifyCounter {
+    std::atomic<long>* slot = &g_verified[g_verify_next_slot.fetch_add(1) % kVerifySlots].n;
+};
+inline void count_verified(long k = 1) { tls_instance<VerifyCounter>().slot->fetch_add(k, std::memory_order_relaxed); }
+}  // namespace
+
+static inline bool verify_fastpath() { return g_verify_fastpath.load(std::memory_order_relaxed); }
+
+void set_verify_fastpath(bool on) { g_verify_fastpath.store(on, std::memory_order_relaxed); }
+bool get_verify_fastpath() { return verify_fastpath(); }
+long verified_decisions() {
+    long s = 0;
+    for (const VerifySlot& v : g_verified) s += v.n.load(std::memory_order_relaxed);
+    return s;
 }
 
 // comparator of sortedChildrenTraversals (node.cpp:356-369, next_probability=false)
@@ -988,6 +1012,7 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
             std::fprintf(stderr, "gz selectChild verification mismatch (depth %d, n %d)\n", depth, n);
             std::abort();
         }
+        count_verified();
     }
     if (chosen != nullptr) path.emplace_back(node, chosen, chosen_best);
     return chosen;
@@ -1348,6 +1373,7 @@ bool PuctEvaluator::spinBuild() {
             spin.reach = reach;
             spin.drift = 1.0;
             spin.valid = true;
+            total_spin_epochs++;
             return true;
         }
         const uint32_t k = (v_end - v0) / 4;
@@ -1402,6 +1428,7 @@ int PuctEvaluator::spinRun(int limit, bool multi) {
                                  r, r2);
                     std::abort();
                 }
+                count_verified();
                 return r2;
             }
         }
@@ -1561,6 +1588,7 @@ int PuctEvaluator::spinRunSlow(int limit, bool verify) {
                 std::fprintf(stderr, "gz spin fast-path: converged() is true\n");
                 std::abort();
             }
+            count_verified();
         } else if (latch) {
             rng.discard((uint64_t)spin.reach);   // the root latch's per-child draws (values unused)
         }

@@ -81,6 +81,7 @@ public:
     long totalEvaluations() const { return total_evaluations; }
     long totalTreePlayouts() const { return total_tree_playouts; }
     long totalTranspositions() const { return total_transpositions; }
+    long totalSpinEpochs() const { return total_spin_epochs; }
 
 private:
     void removeNode(PuctNode*);
@@ -169,6 +170,7 @@ private:
     long total_evaluations = 0;
     long total_tree_playouts = 0;   // diagnostics: NN-free playouts = tree playouts - evaluations
     long total_transpositions = 0;  // diagnostics: edges attached to an existing node (lookup_transpositions)
+    long total_spin_epochs = 0;     // diagnostics: root spin epochs built (spinBuild)
     bool do_playouts = false;
     bool mirror_ok = true;   // every node has one parent: the child mirrors (node.h) are exact
     PlayoutStats stats;
@@ -176,5 +178,10 @@ private:
 };
 
 double get_time();
+
+// GZ_VERIFY_FASTPATH at run time (process-wide; gz_engine_set_verify_fastpath)
+void set_verify_fastpath(bool on);
+bool get_verify_fastpath();
+long verified_decisions();
 
 }  // namespace gz

@@ -28,8 +28,8 @@ static size_t node_bytes(int num_children, int role_count, int num_words) {
 // with 4 KiB pages nearly every cold node visit is also a TLB miss) and recycled per thread by
 // 64-byte size class, without malloc's free lists (whose unlink checks touched cold neighbouring
 // chunks: ~5 % of engine time).  A block freed on another thread joins that thread's lists; a
-// thread's lists pass to a process-wide pool when it exits, and new blocks come from that pool
-// before a fresh chunk.  Chunks live as long as the process; larger nodes use aligned_alloc.
+// thread's lists pass to a process-wide pool when it exits or destroys a pool (node_cache_flush),
+// and new blocks come from that pool before a fresh chunk.  Chunks live as long as the process; larger nodes use aligned_alloc.
 namespace {
 constexpr size_t kNodeCacheClasses = 1024;     // blocks up to 64 KiB come from chunks
 constexpr size_t kChunkBytes = size_t(2) << 20;
@@ -43,21 +43,51 @@ NodePool& node_pool() {
     return *p;
 }
 
+#if defined(__SANITIZE_ADDRESS__)
+// AddressSanitizer builds (tests/test_transpositions.py) keep the recycling allocator: a block on a
+// free list is poisoned whole (its link word too), so a use after free is caught even when the
+// block is recycled; the list code unpoisons a link word only for the access itself.
+#include <sanitizer/asan_interface.h>
+inline void poison(void* p, size_t n) { ASAN_POISON_MEMORY_REGION(p, n); }
+inline void unpoison(void* p, size_t n) { ASAN_UNPOISON_MEMORY_REGION(p, n); }
+#else
+inline void poison(void*, size_t) {}
+inline void unpoison(void*, size_t) {}
+#endif
+
+inline void* link_of(void* p) {
+    unpoison(p, sizeof(void*));
+    void* n = *static_cast<void**>(p);
+    poison(p, sizeof(void*));
+    return n;
+}
+inline void set_link(void* p, void* n) {
+    unpoison(p, sizeof(void*));
+    *static_cast<void**>(p) = n;
+    poison(p, sizeof(void*));
+}
+
 struct NodeCache {
     void* head[kNodeCacheClasses] = {};
+    long blocks = 0;       // blocks on this thread's lists
     char* cur = nullptr;   // bump region of the current chunk
     char* end = nullptr;
-    ~NodeCache() {
+    ~NodeCache() { flush(); }
+    // hand every listed block to the process-wide pool
+    void flush() {
+        if (blocks == 0) return;
         NodePool& pool = node_pool();
         std::lock_guard<std::mutex> lk(pool.mu);
         for (size_t c = 0; c < kNodeCacheClasses; ++c) {
             void* p = head[c];
             if (p == nullptr) continue;
             void* last = p;
-            while (*static_cast<void**>(last) != nullptr) last = *static_cast<void**>(last);
-            *static_cast<void**>(last) = pool.head[c];
+            for (void* n = link_of(last); n != nullptr; n = link_of(last)) last = n;
+            set_link(last, pool.head[c]);
             pool.head[c] = p;
+            head[c] = nullptr;
         }
+        blocks = 0;
     }
     void* fresh(size_t bytes) {
         if (cur == nullptr || (size_t)(end - cur) < bytes) {
@@ -73,27 +103,22 @@ struct NodeCache {
     }
 };
 
-#if defined(__SANITIZE_ADDRESS__)
-// AddressSanitizer builds (tests/test_transpositions.py): every node through malloc, so a use
-// after free is caught instead of landing in a recycled block
-constexpr bool kPooled = false;
-#else
-constexpr bool kPooled = true;
-#endif
-
 void* node_alloc(size_t bytes) {   // bytes: a multiple of 64
     const size_t c = bytes / 64;
-    if (!kPooled || c >= kNodeCacheClasses) return std::aligned_alloc(64, bytes);
+    if (c >= kNodeCacheClasses) return std::aligned_alloc(64, bytes);
     NodeCache& nc = tls_instance<NodeCache>();
     if (void* p = nc.head[c]) {
-        nc.head[c] = *static_cast<void**>(p);
+        nc.head[c] = link_of(p);
+        nc.blocks--;
+        unpoison(p, bytes);
         return p;
     }
-    {   // blocks of exited threads
+    {   // blocks of exited threads / destroyed pools
         NodePool& pool = node_pool();
         std::lock_guard<std::mutex> lk(pool.mu);
         if (void* p = pool.head[c]) {
-            pool.head[c] = *static_cast<void**>(p);
+            pool.head[c] = link_of(p);
+            unpoison(p, bytes);
             return p;
         }
     }
@@ -102,15 +127,22 @@ void* node_alloc(size_t bytes) {   // bytes: a multiple of 64
 
 void node_free(void* p, size_t bytes) {
     const size_t c = bytes / 64;
-    if (!kPooled || c >= kNodeCacheClasses) {
+    if (c >= kNodeCacheClasses) {
         std::free(p);
         return;
     }
     NodeCache& nc = tls_instance<NodeCache>();
-    *static_cast<void**>(p) = nc.head[c];
+    poison(p, bytes);
+    set_link(p, nc.head[c]);
     nc.head[c] = p;
+    nc.blocks++;
 }
 }  // namespace
+
+// A pool torn down on a thread that never runs its games (gz_runner_destroy on the caller's thread)
+// frees every node onto that thread's lists: hand them to the process-wide pool, where the next
+// runner's engine threads find them (instead of growing a second tree footprint).
+void node_cache_flush() { tls_instance<NodeCache>().flush(); }
 
 // node.cpp:111-149: children = cross product of every role's legal moves, role 0 outermost.
 static inline void initChild(PuctNodeChild* child, PuctChildCold* cold, const JointMove& move) {

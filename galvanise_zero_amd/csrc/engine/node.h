@@ -155,4 +155,7 @@ private:
     PuctNode* node;
 };
 
+// Hands the calling thread's recycled node blocks to the process-wide pool (node.cpp).
+void node_cache_flush();
+
 }  // namespace gz

@@ -206,15 +206,35 @@ void SelfPlay::playOnce() {
     resign1_false_positive_check_scores.clear();
 
     const long evals0 = pe->totalEvaluations();
+    const long playouts0 = pe->totalTreePlayouts();
+    const long epochs0 = pe->totalSpinEpochs();
+    coro = coro_current();
+    game_e0 = evals0;
+    game_c0 = coro_cycles_now();
+    int starting_sample_depth = 0;
     auto completed = [&]() {
-        manager->getStats().games_completed++;
-        manager->getStats().completed_game_evals += pe->totalEvaluations() - evals0;
+        PoolStats& st = manager->getStats();
+        st.games_completed++;
+        st.completed_game_evals += pe->totalEvaluations() - evals0;
+        OrdinalStats& o = st.ord;
+        const int k = std::min(match_count, OrdinalStats::kOrdinals) - 1;
+        const uint64_t cyc = coro_cycles_now() - game_c0;
+        o.games[k]++;
+        o.evals[k] += pe->totalEvaluations() - evals0;
+        o.tree_playouts[k] += pe->totalTreePlayouts() - playouts0;
+        o.moves[k] += pe->getRootNode()->game_depth - starting_sample_depth;
+        o.spin_epochs[k] += pe->totalSpinEpochs() - epochs0;
+        o.cycles[k] += cyc;
+        const double ms = (double)cyc / tsc_hz() * 1e3;
+        int b = 0;
+        while (b < OrdinalStats::kHist - 1 && ms >= (double)(1L << b)) ++b;
+        o.cost_hist[b]++;
     };
 
     pe->reset(0);
     PuctNode* node = pe->establishRoot(initial_state);
     GZ_ASSERT(!node->isTerminal());
-    const int starting_sample_depth = node->game_depth;
+    starting_sample_depth = node->game_depth;
 
     node = collectSamples(node);
     if (game_samples.empty()) {
@@ -324,6 +344,22 @@ void SelfPlayManager::startSelfPlayers(const SelfPlayConfig* config) {
         self_plays.push_back(sp);
         scheduler->addRunnable([sp]() { sp->playGamesForever(); });
     }
+}
+
+void SelfPlayManager::inflight(long* games, double* engine_s, long* evals) const {
+    long g = 0, e = 0;
+    uint64_t c = 0;
+    for (size_t i = 0; i < self_plays.size(); ++i) {
+        const SelfPlay* sp = self_plays[i];
+        if (sp->coro == nullptr) continue;
+        g++;
+        const uint64_t now = sp->coro->cycles;   // as of the coroutine's last switch
+        if (now > sp->game_c0) c += now - sp->game_c0;
+        e += evaluators[i]->totalEvaluations() - sp->game_e0;
+    }
+    *games = g;
+    *engine_s = (double)c / tsc_hz();
+    *evals = e;
 }
 
 void SelfPlayManager::poll() {

@@ -92,6 +92,26 @@ private:
     std::vector<float> resign0_false_positive_check_scores;
     std::vector<float> resign1_false_positive_check_scores;
     Rng rng;
+
+public:
+    // the game in progress (diagnostics, read racily by stats snapshots): its coroutine, and the
+    // coroutine's TSC cycles / the evaluator's evaluations when it started
+    const Coro* coro = nullptr;
+    uint64_t game_c0 = 0;
+    long game_e0 = 0;
+};
+
+// Per-game cost by the game's ordinal within its slot (1st, 2nd, ... game a SelfPlay plays; the
+// last bucket holds every later one): is a slot's k-th game more expensive than its first?
+struct OrdinalStats {
+    static constexpr int kOrdinals = 8, kHist = 32;
+    long games[kOrdinals] = {};
+    long evals[kOrdinals] = {};
+    long tree_playouts[kOrdinals] = {};
+    long moves[kOrdinals] = {};
+    long spin_epochs[kOrdinals] = {};
+    uint64_t cycles[kOrdinals] = {};
+    long cost_hist[kHist] = {};    // completed games by engine milliseconds, [2^(k-1), 2^k) ms
 };
 
 struct PoolStats {
@@ -111,6 +131,7 @@ struct PoolStats {
     long completed_game_evals = 0; // NN evaluations consumed by the games counted in games_completed
     long tree_playouts = 0;        // tree playouts of every game of the pool (filled by treePlayouts())
     long transpositions = 0;       // transposition edges attached (filled by transpositions())
+    OrdinalStats ord;
 };
 
 class SelfPlayManager {
@@ -147,6 +168,9 @@ public:
 
     void startSelfPlayers(const SelfPlayConfig* config);
     void poll();
+
+    // games in progress: count, engine seconds and evaluations they have used so far
+    void inflight(long* games, double* engine_s, long* evals) const;
 
     std::vector<Sample*>& getSamples() { return samples; }
     ReadyEvent* getReadyEvent() { return &ready_event; }

@@ -126,7 +126,10 @@ struct gz_runner {
     // pool's batch is split, so every batch runs on one network
     std::mutex roll_m;
     std::condition_variable roll_cv;
-    std::atomic<int> roll_state{0};  // 0 none, 1 pending, 2 applied, -1 failed
+    // 0 none, 1 pending, 3 claimed by the launcher (applying), 2 applied, -1 failed.  The launcher
+    // claims a pending roll (1 -> 3) before reading roll_blob; a timed-out caller withdraws it
+    // (1 -> 0) before its blob can be freed, or waits for a claimed one to finish.
+    std::atomic<int> roll_state{0};
     const float* roll_blob = nullptr;
     size_t roll_count = 0;
     int roll_device = 0, roll_clear = 0;
@@ -332,7 +335,8 @@ static void launcher_main(gz_runner* r) {
                     for (size_t i = 0; i < r->pools.size(); ++i) r->roll_batches[i] = r->pools[i].launched;
                 }
             }
-            if (!split_pending) apply_roll(r, launches_issued);
+            int pending = 1;
+            if (!split_pending && r->roll_state.compare_exchange_strong(pending, 3)) apply_roll(r, launches_issued);
         }
         // gather waiting pools into one segmented launch
         Batch& b = r->batches_ring[next_slot];
@@ -375,13 +379,17 @@ static void launcher_main(gz_runner* r) {
                 // (re-stamped, so it waits for more rows like a newly queued pool).  Fewer rows
                 // than one round, or a queue nothing can join (all_waiting), launch whole.
                 int target = std::min(queued, max_rows);
-                // (a pending generation roll waits for a launch that splits no pool)
-                if (wave_rows > 0 && target > wave_rows && !all_waiting && r->roll_state.load() != 1)
+                // a pending generation roll waits for a launch that splits no pool: while one is
+                // pending, launches end at a whole-pool boundary (also when max_launch_rows is what
+                // limits them), so the queue front soon holds no split pool
+                const bool roll_pending = r->roll_state.load() == 1;
+                if (wave_rows > 0 && target > wave_rows && !all_waiting && !roll_pending)
                     target = (target / wave_rows) * wave_rows;
                 while (!r->queue.empty() && b.rows < target && (int)b.parts.size() < GZ_MAX_SEGMENTS) {
                     const int i = r->queue.front();
                     Pool& p = r->pools[i];
                     const int take = std::min(p.rows - p.sub, target - b.rows);
+                    if (roll_pending && take < p.rows - p.sub && !b.parts.empty()) break;
                     const bool last = p.sub + take == p.rows;
                     b.parts.push_back(Part{i, p.sub, take, last});
                     b.rows += take;
@@ -803,15 +811,20 @@ extern "C" int gz_runner_update_network(gz_runner* r, const float* blob, size_t 
     r->roll_state = 1;
     r->qcv.notify_all();
     const auto t0 = std::chrono::steady_clock::now();
-    while (r->roll_state.load() == 1) {
+    while (r->roll_state.load() == 1 || r->roll_state.load() == 3) {
         r->roll_cv.wait_for(lk, std::chrono::milliseconds(2));
-        if (r->failed.load()) {
-            g_err = r->fail_msg;
-            return -1;
-        }
-        if (timeout_s > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
-            g_err = "timeout waiting for the launcher to apply the generation roll";
-            return -2;
+        const bool timed_out =
+            timeout_s > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s;
+        if (r->failed.load() || timed_out) {
+            // withdraw the roll before returning (the caller may free the blob); one the launcher
+            // has already claimed is waited for -- apply_roll takes no unbounded wait
+            int pending = 1;
+            if (r->roll_state.compare_exchange_strong(pending, 0)) {
+                r->roll_blob = nullptr;
+                g_err = r->failed.load() ? r->fail_msg : "timeout waiting for the launcher to apply the generation roll";
+                return r->failed.load() ? -1 : -2;
+            }
+            if (r->roll_state.load() == 3) continue;   // being applied: finishes shortly
         }
     }
     r->roll_blob = nullptr;
@@ -821,6 +834,21 @@ extern "C" int gz_runner_update_network(gz_runner* r, const float* blob, size_t 
         return -1;
     }
     r->roll_state = 0;
+    return 0;
+}
+
+// Per-ordinal game costs summed over the runner's pools (gzero_engine.h gz_ordinal_stats).
+extern "C" int gz_runner_ordinal_stats(gz_runner* r, gz_ordinal_stats* out) {
+    if (!r || !out) {
+        g_err = "null argument";
+        return -1;
+    }
+    std::memset(out, 0, sizeof(*out));
+    for (Pool& p : r->pools)
+        if (p.pool && gz_pool_add_ordinal_stats(p.pool, out) != 0) {
+            g_err = gz_engine_last_error();
+            return -1;
+        }
     return 0;
 }
 

@@ -22,7 +22,10 @@ Heads (both):
 * value:  ``conv2d_block(1, 1, do_bn=False)`` -> act -> Flatten -> Dense(hidden, act)
   -> Dense(V, softmax)                                                     (model.py:273-291);
   with ``global_pooling_value`` the value 1x1 conv has BN and the flat features are
-  [GlobalAveragePooling(trunk) (F), conv (HW)] concatenated in that order (model.py:262-271)
+  [GlobalAveragePooling(trunk) (F), conv (HW)] concatenated in that order (model.py:262-271);
+  with ``concat_all_layers`` (v2 only) every trunk layer -- the initial conv block's output and each
+  residual block's add -- gets its own ``conv2d_block(1, 1)`` (conv + BN + act), and the flat
+  features are those B + 1 maps of HW values concatenated in layer order (model.py:251-260)
 
 BatchNormalization is inference-mode with epsilon 1e-3 (Keras default; every
 ``data/*/models/*.json`` records ``epsilon: 0.001``).
@@ -72,6 +75,8 @@ class NetDesc:
     # initial conv kernel: 0 = model.py's (1 for v2, cnn_kernel_size for v1); some v2 model files
     # (e.g. data/hexLG13/models/b4_305.json) have a 3x3 initial conv + BN + act
     initial_kernel_size: int = 0
+    # value head over every trunk layer (model.py:251-260; v2 only, e.g. data/hex19/models/h2_477.json)
+    concat_all_layers: bool = False
 
     @property
     def initial_kernel(self):
@@ -81,7 +86,10 @@ class NetDesc:
 
     @property
     def value_features(self):
-        """Inputs of the value hidden Dense: [GAP (F)] + the value conv's HW."""
+        """Inputs of the value hidden Dense: [GAP (F)] + the value conv's HW, or (B + 1) HW with
+        concat_all_layers."""
+        if self.concat_all_layers:
+            return (self.residual_layers + 1) * self.hw
         return (self.cnn_filter_size if self.global_pooling_value else 0) + self.hw
 
     @property
@@ -106,7 +114,8 @@ class NetDesc:
         F, C, HW, k, k0 = self.cnn_filter_size, self.input_channels, self.hw, self.cnn_kernel_size, self.initial_kernel
         f = 2 * HW * C * F * k0 * k0 + self.residual_layers * 2 * (2 * HW * F * F * k * k)
         f += self.residual_layers * 2 * (2 * F * self.se_units)
-        return f + (2 * self.role_count + 1) * 2 * HW * F
+        value_convs = self.residual_layers + 1 if self.concat_all_layers else 1
+        return f + (2 * self.role_count + value_convs) * 2 * HW * F
 
     def flops_heads(self):
         """FLOPs of the heads kernel per evaluation: the dense layers."""
@@ -150,9 +159,14 @@ def weight_spec(d: NetDesc) -> List[Tuple[str, Tuple[int, ...]]]:
         bn("policy%d_bn" % r, 2)
         spec.append(("policy%d_dense" % r, (2 * d.hw, p)))
         spec.append(("policy%d_bias" % r, (p,)))
-    conv("value_conv", (1, 1, F, 1))
-    if d.value_bn:
-        bn("value_bn", 1)
+    if d.concat_all_layers:                  # one conv2d_block(1, 1) per trunk layer (model.py:251-260)
+        for j in range(d.residual_layers + 1):
+            conv("value%d_conv" % j, (1, 1, F, 1))
+            bn("value%d_bn" % j, 1)
+    else:
+        conv("value_conv", (1, 1, F, 1))
+        if d.value_bn:
+            bn("value_bn", 1)
     spec.append(("value_hidden", (d.value_features, d.value_hidden_size)))
     spec.append(("value_hidden_bias", (d.value_hidden_size,)))
     spec.append(("value_dense", (d.value_hidden_size, d.num_values)))

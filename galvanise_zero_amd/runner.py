@@ -96,6 +96,20 @@ class SelfPlayRunner(object):
         self.lib.gz_runner_stats_get(self.handle, ctypes.byref(st))
         return st.as_dict()
 
+    def ordinal_stats(self):
+        """Per-game costs by the game's ordinal within its slot (gz_ordinal_stats)."""
+        st = _native.GzOrdinalStats()
+        if self.lib.gz_runner_ordinal_stats(self.handle, ctypes.byref(st)) != 0:
+            raise RuntimeError("gz_runner_ordinal_stats: %s" % self.lib.gz_runner_last_error().decode())
+        return st.as_dict()
+
+    @staticmethod
+    def set_verify_fastpath(on):
+        """Re-check every engine fast-path decision against the literal reference path from now on
+        (process-wide, GZ_VERIFY_FASTPATH at run time; a mismatch aborts the process).  Returns
+        the previous setting."""
+        return _native.set_verify_fastpath(on)
+
     def stop(self):
         if self.handle:
             rc = self.lib.gz_runner_stop(self.handle)
@@ -149,6 +163,13 @@ class GamePool(object):
     def fetch_samples(self):
         s = _native.take_string(self.lib.gz_pool_fetch_samples(self.handle))
         return json.loads(s) if s else []
+
+    def ordinal_stats(self):
+        """Per-game costs by the game's ordinal within its slot (gz_ordinal_stats)."""
+        st = _native.GzOrdinalStats()
+        if self.lib.gz_pool_add_ordinal_stats(self.handle, ctypes.byref(st)) != 0:
+            raise RuntimeError("gz_pool_add_ordinal_stats: %s" % _native.engine_error())
+        return st.as_dict()
 
     def stats(self):
         st = _native.GzPoolStats()

@@ -99,6 +99,24 @@ typedef struct gz_pool_stats {
     long transpositions;         /* edges attached to an existing node (lookup_transpositions) */
 } gz_pool_stats;
 
+/* Per-game cost by the game's ordinal within its slot (a slot = one SelfPlay of a pool; its 1st,
+ * 2nd, ... game; the last bucket holds every later game), for the steady-state analysis (DESIGN.md
+ * section 6).  Build diagnostics: the reference has no counterpart. */
+#define GZ_ORDINALS 8
+#define GZ_COST_HIST 32
+typedef struct gz_ordinal_stats {
+    long games[GZ_ORDINALS];          /* completed games */
+    long evals[GZ_ORDINALS];          /* NN evaluations they used */
+    long tree_playouts[GZ_ORDINALS];  /* tree playouts (NN-free ones included) */
+    long moves[GZ_ORDINALS];          /* moves played */
+    long spin_epochs[GZ_ORDINALS];    /* root spin epochs built (engine fast path) */
+    double engine_s[GZ_ORDINALS];     /* engine-thread seconds inside the games' coroutines (TSC) */
+    long cost_hist[GZ_COST_HIST];     /* completed games by engine ms: bucket k = [2^(k-1), 2^k) ms */
+    long inflight_games;              /* games in progress at the snapshot */
+    double inflight_engine_s;         /* engine seconds they have used so far */
+    long inflight_evals;              /* evaluations they have used so far */
+} gz_ordinal_stats;
+
 const char* gz_engine_last_error(void);
 void gz_free(void* p);                         /* frees strings returned by this library */
 
@@ -184,6 +202,16 @@ int gz_pool_get_stats(gz_pool* p, gz_pool_stats* out);
 int gz_pool_clear_unique_states(gz_pool* p);
 char* gz_pool_fetch_samples(gz_pool* p);          /* JSON or NULL; free with gz_free */
 long gz_pool_take_sample_count(gz_pool* p);       /* drops queued samples, returns how many */
+/* adds the pool's per-ordinal counters into *out (zero it first to read one pool) */
+int gz_pool_add_ordinal_stats(gz_pool* p, gz_ordinal_stats* out);
+
+/* ---- run-time verification of the engine's fast paths (build diagnostics) -------------------- */
+/* on = 1: every sort-free selection, spin playout and register spin run is re-checked against the
+ * literal reference path, aborting on a difference (what GZ_VERIFY_FASTPATH=1 sets at load);
+ * process-wide, takes effect at the next decision; returns the previous setting. */
+int gz_engine_set_verify_fastpath(int on);
+/* fast-path decisions re-checked so far (process-wide) */
+long gz_engine_verified_decisions(void);
 char* gz_pool_fetch_samples_n(gz_pool* p, long* count);  /* as fetch_samples, *count = records */
 
 #ifdef __cplusplus

@@ -44,7 +44,11 @@ typedef struct gz_net_desc {
      *   GZ_PRECISION_SPLIT (3): fp32 accuracy -- each fp32 operand as bf16 hi + bf16 lo and each
      *   product as hi*hi + hi*lo + lo*hi on the MFMA (~16 significant bits per operand, fp32
      *   accumulation); F <= 128 on boards <= 64 positions, F = 256 on boards <= 13 x 13 (single
-     *   image; 13 x 13 by two passes per conv).  The heads are fp32 in both modes. */
+     *   image; 13 x 13 by two passes per conv).  The heads' 1x1 convs, softmaxes and value MLP are
+     *   fp32 in both modes; the policy Dense is fp32 except for single-image nets with a policy of
+     *   >= 512 moves (amazons), whose policy Dense of the whole launch runs as one bf16x3 split MFMA
+     *   GEMM in both modes (policy_gemm_kernel; GZ_NO_GEMM_HEADS=1 keeps it fp32 on the VALU).
+     *   Stated error per config: galvanise_zero_amd/nn/tolerance.py. */
     int precision;
     /* v2 (pre-activation) trunk, model.py:78-151 (the reference's features=True templates and its
      * non-legacy model files); all zero = v1. */
@@ -220,6 +224,10 @@ int gz_runner_update_network(gz_runner* r, const float* blob, size_t count, int 
 /* After a roll: pool_batches[i] = batches of pool i launched on the previous network;
  * *launches_before = launches issued before the swap. */
 int gz_runner_roll_info(gz_runner* r, long* pool_batches, int npools, long* launches_before);
+/* Per-game costs by the game's ordinal within its slot, summed over the runner's pools (struct
+ * gz_ordinal_stats, include/gzero_engine.h); a snapshot, safe while the runner runs. */
+struct gz_ordinal_stats;
+int gz_runner_ordinal_stats(gz_runner* r, struct gz_ordinal_stats* out);
 const char* gz_runner_last_error(void);
 
 #ifdef __cplusplus

@@ -23,6 +23,9 @@ executed by Keras 2.2 / TF 1.12 ``predict_on_batch`` (``src/ggpzero/util/cppinte
   bias) -> multiply), add without activation (:147); dropout is the identity at inference.
 * ``global_pooling_value`` model.py:262-271: value features = concat(GAP(trunk) [F], flatten(value
   1x1 conv + BN + act) [HW]).
+* ``concat_all_layers`` model.py:251-260 (v2 only: ``all_layers`` is built by the v2 branch,
+  :173-198): value features = concat over the trunk layers (initial conv block output, then each
+  residual block's add) of flatten(1x1 conv(1) + BN + act) [HW each], in layer order.
 
 Arithmetic is float64 (the fp32 TF result is within ~1e-6 of it); outputs are float32 like
 ``predict_on_batch``.  Parity of the reference NN itself is *unpinned*: no reference test holds a
@@ -100,6 +103,7 @@ def forward(desc, weights, planes, logits=False):
     x = conv(x, "initial_conv")
     if not v2 or desc.initial_bn:
         x = _act(_bn(x, w, "initial_bn"), leaky)
+    layers = [x]                                                   # all_layers, model.py:181,198
     for i in range(desc.residual_layers):
         t = x
         if v2:
@@ -114,19 +118,24 @@ def forward(desc, weights, planes, logits=False):
             y = _act(_bn(conv(x, "res%d_conv0" % i), w, "res%d_bn0" % i), leaky)
             y = _bn(conv(y, "res%d_conv1" % i), w, "res%d_bn1" % i)
             x = _act(t + y, leaky)
+        layers.append(x)
     outs = []
     for r in range(desc.role_count):
         h = _act(_bn(conv(x, "policy%d_conv" % r), w, "policy%d_bn" % r), leaky)
         logits_r = _flatten(h, desc.flatten_nchw) @ w["policy%d_dense" % r].astype(np.float64)
         logits_r = logits_r + w["policy%d_bias" % r]
         outs.append(logits_r if logits_out else _softmax(logits_r).astype(np.float32))
-    v = conv(x, "value_conv")
-    if getattr(desc, "value_bn", False):
-        v = _bn(v, w, "value_bn")
-    v = _act(v, leaky)
-    flat = _flatten(v, desc.flatten_nchw)
-    if getattr(desc, "global_pooling_value", False):
-        flat = np.concatenate([x.mean(axis=(1, 2)), flat], axis=1)
+    if getattr(desc, "concat_all_layers", False):
+        flat = np.concatenate([_flatten(_act(_bn(conv(l, "value%d_conv" % j), w, "value%d_bn" % j), leaky),
+                                        desc.flatten_nchw) for j, l in enumerate(layers)], axis=1)
+    else:
+        v = conv(x, "value_conv")
+        if getattr(desc, "value_bn", False):
+            v = _bn(v, w, "value_bn")
+        v = _act(v, leaky)
+        flat = _flatten(v, desc.flatten_nchw)
+        if getattr(desc, "global_pooling_value", False):
+            flat = np.concatenate([x.mean(axis=(1, 2)), flat], axis=1)
     hid = _act(flat @ w["value_hidden"].astype(np.float64) + w["value_hidden_bias"], leaky)
     val = hid @ w["value_dense"].astype(np.float64) + w["value_bias"]
     outs.append(val if logits_out else _value_out(desc, val))

@@ -930,6 +930,7 @@ class Manager(object):
         self.samples = []
         self.stats = dict(dupes=0, resigns=0, no_samples=0, aborts_game_length=0, early_run_to_ends=0)
         self.evaluators = []
+        self.self_plays = []
 
     def create_sample(self, node):
         rc = self.sm.role_count
@@ -966,6 +967,7 @@ class Manager(object):
             pe.rng.seed(S.rng_mix(self.seed, gi, 0))
             self.evaluators.append(pe)
             sp = SelfPlay(self, conf, pe, "%s_%d" % (self.identifier, ii), S.rng_mix(self.seed, gi, 1))
+            self.self_plays.append(sp)
             self.scheduler.add_runnable(sp.play_games_forever())
 
     def poll(self, pred_count, policies, values):

@@ -138,3 +138,51 @@ def test_torch_cpu_fp32_matches_oracle(desc):
     for a, b in zip(TorchCPUNet(desc, w).predict_on_batch(x), nn_ref.forward(desc, w, x)):
         assert a.dtype == np.float32 and a.shape == b.shape
         assert float(np.abs(a - b).max()) < 2e-5
+
+
+ORACLE_DESCS = {
+    "v1": NetDesc(5, 8, 8, 32, 2, [17, 19], value_hidden_size=16),
+    "v1_legacy_leaky": NetDesc(5, 6, 6, 16, 1, [9, 9], value_hidden_size=8, conv_bias=True, value_bn=True,
+                               value_sigmoid=True, flatten_nchw=True, leaky_relu=True),
+    "v2_se_gap": NetDesc(5, 7, 7, 24, 2, [11, 13], value_hidden_size=8, num_values=3, resnet_v2=True, se_units=9,
+                         global_pooling_value=True, value_bn=True),
+    "v2_concat": NetDesc(5, 7, 6, 16, 3, [11, 13], value_hidden_size=8, resnet_v2=True, concat_all_layers=True),
+}
+
+
+@pytest.mark.parametrize("name", list(ORACLE_DESCS))
+def test_torch_f64_oracle_matches_numpy_oracle(name):
+    """oracle/nn_ref_torch.py (float64 torch, the GPU-side oracle of tools/split_error_dist.py)
+    restates oracle/nn_ref.forward: equal to ~1e-12 on the CPU, probabilities and logits."""
+    from oracle import nn_ref_torch
+    desc = ORACLE_DESCS[name]
+    w = random_weights(desc, 3, bias_std=0.2)
+    x = random_planes(desc, 7, 4)
+    for logits in (False, True):
+        a = nn_ref.forward(desc, w, x, logits=logits)
+        b = nn_ref_torch.forward(desc, w, x, logits=logits)
+        for u, v in zip(a, b):
+            assert u.shape == v.shape
+            assert np.abs(u.astype(np.float64) - v.astype(np.float64)).max() <= (1e-7 if not logits else 1e-10)
+
+
+def test_concat_all_layers_value_head_semantics():
+    """model.py:251-260: the value Dense reads (B + 1) HW features in layer order, layer j's block
+    its own 1x1 conv + BN + act.  Wiring check: with layer j's rows of value_hidden zeroed, the value
+    no longer depends on layer j's conv (and does on every other layer's)."""
+    desc = ORACLE_DESCS["v2_concat"]
+    spec = dict(weight_spec(desc))
+    B, hw = desc.residual_layers, desc.hw
+    assert spec["value_hidden"] == ((B + 1) * hw, desc.value_hidden_size)
+    assert all("value%d_conv" % j in spec for j in range(B + 1)) and "value_conv" not in spec
+    assert desc.flops_trunk() - NetDesc(**{**desc.__dict__, "concat_all_layers": False}).flops_trunk() == B * 2 * hw * 16
+    w = random_weights(desc, 3)
+    x = random_planes(desc, 5, 4)
+    for j in range(B + 1):
+        wz = [(k, a.copy()) for k, a in w]
+        dict(wz)["value_hidden"][j * hw:(j + 1) * hw] = 0.0
+        base = nn_ref.forward(desc, wz, x, logits=True)[-1]
+        for jj in range(B + 1):
+            wp = [(k, a * 1.7 if k == "value%d_conv" % jj else a) for k, a in wz]
+            moved = not np.allclose(nn_ref.forward(desc, wp, x, logits=True)[-1], base, rtol=0, atol=1e-12)
+            assert moved == (jj != j), (j, jj)
