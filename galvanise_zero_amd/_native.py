@@ -59,7 +59,8 @@ class GzNetDesc(ctypes.Structure):
                 ("initial_kernel", ctypes.c_int),
                 ("initial_bn", ctypes.c_int),
                 ("se_units", ctypes.c_int),
-                ("global_pooling_value", ctypes.c_int)]
+                ("global_pooling_value", ctypes.c_int),
+                ("concat_all_layers", ctypes.c_int)]
 
 GZ_PRECISION_BF16 = 1
 GZ_PRECISION_SPLIT = 3
@@ -136,6 +137,7 @@ def make_net_desc(desc, precision=GZ_PRECISION_BF16):
     d.initial_bn = int(getattr(desc, "initial_bn", True))
     d.se_units = int(getattr(desc, "se_units", 0))
     d.global_pooling_value = int(getattr(desc, "global_pooling_value", False))
+    d.concat_all_layers = int(getattr(desc, "concat_all_layers", False))
     return d
 
 

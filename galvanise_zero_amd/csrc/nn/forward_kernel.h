@@ -105,6 +105,15 @@ struct KParams {
     int btab_off;            // LDS byte offset of the trunk bias table
     int se_off;              // LDS byte offset of the squeeze-excite scratch
     int P[kMaxRoles];
+    int VK;                  // value hidden Dense inputs per board: gapF + npos, or cal * npos
+    // concat_all_layers value head (v2, model.py:251-260): cal = B + 1 trunk layers, each through a
+    // 1x1 conv (BN folded: wcl [cal][F], bcl [cal]) + act; the trunk writes those features to the
+    // device scratch as it goes and the dense heads run in heads_kernel (nofuse)
+    int cal;
+    const float* wcl;
+    const float* bcl;
+    int cal_off;             // LDS byte offset of the per-wave partial sums [4][NB][npos]
+    int nofuse;              // two-image kernels: features to the device scratch, no fused heads
 };
 
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
@@ -824,6 +833,45 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     // P = 2: this workgroup's lo image, after the grid's residual scratch
     char* xlo = P == 2 ? (char*)kp.resid + (size_t)gridDim.x * G::RESID_BYTES + (size_t)blockIdx.x * G::LO_BYTES : nullptr;
 
+    // concat_all_layers value head (V2 nets, model.py:251-260): trunk layer j's 1x1 value conv from
+    // the fp32 stream in acc -- per-wave partial sums of board bb into LDS (cal_partial), summed in a
+    // fixed order, biased and activated after the next workgroup barrier (cal_reduce) into the
+    // device feature scratch, which heads_kernel reads.  The partials are rewritten only after at
+    // least one more barrier (the next block's first epilogue), so one buffer serves every layer.
+    float* calp = (float*)(smem + kp.cal_off);   // [4 waves][NB][NPOS]
+    auto cal_partial = [&](int j, int bb) {
+        float4 wv[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) wv[ct] = *(const float4*)(kp.wcl + (size_t)j * F + co_base + 16 * ct + 4 * g);
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) {
+            float sum = 0.f;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const f32x4 a = acc[ct][bb * PT + pt];
+                sum += a[0] * wv[ct].x;
+                sum += a[1] * wv[ct].y;
+                sum += a[2] * wv[ct].z;
+                sum += a[3] * wv[ct].w;
+            }
+            sum += __shfl_xor(sum, 16, 64);
+            sum += __shfl_xor(sum, 32, 64);
+            const int p = 16 * pt + li;
+            if (g == 0 && p < NPOS) calp[(wave * NB + bb) * NPOS + p] = sum;
+        }
+    };
+    auto cal_reduce = [&](int j) {
+        for (int i = tid; i < NB * NPOS; i += kThreads) {
+            const int bb = i / NPOS, p = i - bb * NPOS;
+            const int board = board0 + bb;
+            if (board >= kp.n) continue;
+            float sum = kp.bcl[j];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) sum += calp[(w * NB + bb) * NPOS + p];
+            kp.feat[(size_t)board * kp.FS + 2 * kp.R * NPOS + j * NPOS + p] = act_fn(sum, kp.leaky);
+        }
+    };
+
     for (int i = threadIdx.x; i < 2 * kp.B * F; i += kThreads * WG) btab[i] = kp.bres[i];
     for (int i = tid; i < NB * G::ZROWS * G::ROWS / 4; i += kThreads) {
         const int bb = i / (G::ZROWS * G::ROWS / 4), j = i % (G::ZROWS * G::ROWS / 4);
@@ -944,6 +992,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                 store_act<F, PTN, P, !G::SI>(X0 + bb * ACT, 16 * pt + li, co, preact ? pre_act(v, psc, psh, kp.leaky) : v, NPOS);
             }
         }
+        if constexpr (V2)
+            if (kp.cal) cal_partial(0, bb);   // layer 0: the initial conv block's output
         __syncthreads();    // scratch is reused by the next board
         if constexpr (P == 2) save_lo_write_hi<F, PTN>(X0, xlo, acc, NPOS, tid, co_base, li, g);
     }
@@ -952,6 +1002,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         ((uint32_t*)(X1 + bb * ACT + NPOS * G::ROWS))[j] = 0u;
     }
     __syncthreads();
+    if constexpr (V2)
+        if (kp.cal) cal_reduce(0);
 
     GZ_STAMP(1);
     // ---- residual tower ------------------------------------------------------------------
@@ -1005,7 +1057,11 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                         if (more) store_act<F, PTN, P, !G::SI>(X0, 16 * t + li, co, pre_act(v, psc, psh, kp.leaky), NPOS);
                     }
                 }
+                if (kp.cal)   // layer blk + 1: the block's add
+#pragma unroll
+                    for (int bb = 0; bb < NB; ++bb) cal_partial(blk + 1, bb);
                 __syncthreads();
+                if (kp.cal) cal_reduce(blk + 1);
                 continue;
             }
 #pragma unroll
@@ -1092,7 +1148,11 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                     if (more) store_act<F, PTN, P, !G::SI>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, pre_act(v, psc, psh, kp.leaky), NPOS);
                 }
             }
+            if (kp.cal)   // layer blk + 1: the block's add
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) cal_partial(blk + 1, bb);
             __syncthreads();
+            if (kp.cal) cal_reduce(blk + 1);
             continue;
         }
 #pragma unroll
@@ -1129,7 +1189,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     // ---- the heads' 1x1 convs (2 per policy role + 1 value) from the fp32 residual stream (a copy
     // of the last epilogue's output is in acc);
     // features in the model's Flatten order go to the scratch for heads_kernel ----------------
-    const int HC = 2 * kp.R + 1;
+    const int HC = 2 * kp.R + (kp.cal ? 0 : 1);   // (concat_all_layers: the value features are written)
     float* hpart = (float*)SCR;                                  // [4][HC][NPOS]
     // the heads' 1x1 conv weights of this wave's channels, loaded together once for the NB boards
     // (two-role games, F <= 128) instead of one dependent global load per conv and board
@@ -1150,13 +1210,14 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     // (WG = 2: each group's 1x1 partials in its own scratch, the features of the workgroup's boards
     // in group 0's, after its partials)
     constexpr bool FUSE = !SI;
+    const bool fuse = FUSE && !kp.nofuse;   // nofuse: the features go to the device scratch
     constexpr int NBW = NB * WG;     // boards per workgroup
     float* fk = (float*)(SCR0 + align16(4 * HC * NPOS * 4));
     float* lg = fk + align16(kp.FS * NBW * 4) / 4;
     // feature k of board bb
     auto feat_at = [&](int bb, int k) -> float& {
-        if constexpr (FUSE) return fk[k * NBW + grp * NB + bb];
-        else return kp.feat[(size_t)(board0 + bb) * kp.FS + k];
+        if (fuse) return fk[k * NBW + grp * NB + bb];
+        return kp.feat[(size_t)(board0 + bb) * kp.FS + k];
     };
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
@@ -1227,7 +1288,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         __syncthreads();    // hpart is reused by the next board
     }
     GZ_STAMP(3);
-    if constexpr (FUSE) {
+    if (fuse) {
         const int wb0 = blockIdx.x * NBW;
         const int nb = kp.n - wb0 < NBW ? kp.n - wb0 : NBW;
         dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);
@@ -1327,7 +1388,7 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
 
     // value head: Dense([GAP F] + HW -> VH) + act, Dense(VH -> V) + softmax
     {
-        const int VH = kp.VH, VK = kp.gapF + NPOS;
+        const int VH = kp.VH, VK = kp.VK;
         const float* fv = fk + (size_t)2 * kp.R * NPOS * BPW;
         for (int j = tid; j < VH; j += NT) {
             float a[BPW];
@@ -1376,7 +1437,7 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
 // LDS of the fused heads (trunk kernels with two activation images): 1x1-conv partials, features,
 // dense outputs
 __host__ __device__ inline int fused_heads_bytes(int npos, int R, int maxP, int VH, int gapF, int nb) {
-    const int FS = (2 * R + 1) * npos + gapF;
+    const int FS = (2 * R + 1) * npos + gapF;   // (concat_all_layers nets never fuse the heads)
     const int LMAX = maxP > VH ? maxP : VH;
     return align16(4 * (2 * R + 1) * npos * 4) + align16(FS * nb * 4) + align16(nb * LMAX * 4);
 }
@@ -1462,8 +1523,7 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
 
 #endif
 
-__host__ inline int heads_lds_bytes(int npos, int R, int maxP, int VH, int gapF) {
-    const int FS = (2 * R + 1) * npos + gapF;
+__host__ inline int heads_lds_bytes(int FS, int maxP, int VH) {
     const int LMAX = maxP > VH ? maxP : VH;
     return (FS * kHeadBoards + kHeadBoards * LMAX + kHeadBoards * 4) * 4;
 }

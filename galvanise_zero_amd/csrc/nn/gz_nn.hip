@@ -46,6 +46,7 @@ struct gz_net {
         int smem = 0;              // dynamic LDS bytes
         int btab_off = 0;          // LDS offset of the bias table
         int se_off = 0;            // LDS offset of the squeeze-excite scratch
+        int cal_off = 0;           // LDS offset of the concat_all_layers partial sums
         bool fused_heads = false;  // the dense heads run inside the trunk kernel (no heads_kernel launch)
         int resid_bytes = 0;       // global residual scratch per workgroup
         int threads = 256;         // workgroup size (512: two wave groups)
@@ -113,6 +114,13 @@ static int initial_kernel(const gz_net_desc& d) {
 }
 static bool has_initial_bn(const gz_net_desc& d) { return !d.resnet_v2 || d.initial_bn; }
 static int gap_features(const gz_net_desc& d) { return d.global_pooling_value ? d.cnn_filter_size : 0; }
+// trunk layers the concat_all_layers value head reads (model.py:251-260), 0 for the other heads
+static int cal_layers(const gz_net_desc& d) { return d.concat_all_layers ? d.residual_layers + 1 : 0; }
+// value hidden Dense inputs
+static int value_features(const gz_net_desc& d) {
+    const int HW = d.input_columns * d.input_rows;
+    return d.concat_all_layers ? cal_layers(d) * HW : gap_features(d) + HW;
+}
 
 // float count of the canonical blob: galvanise_zero_amd/nn/desc.py weight_spec
 static size_t spec_count(const gz_net_desc& d) {
@@ -123,8 +131,9 @@ static size_t spec_count(const gz_net_desc& d) {
     const size_t blk = d.resnet_v2 ? 4 * F + conv + 4 * F + conv + 2 * F * (size_t)d.se_units : 2 * (conv + 4 * F);
     n += (size_t)d.residual_layers * blk;
     for (int r = 0; r < d.role_count; ++r) n += F * 2 + cb * 2 + 4 * 2 + 2 * HW * d.policy_dist_count[r] + d.policy_dist_count[r];
-    n += F + cb + (d.value_bn ? 4 : 0);
-    n += (gap_features(d) + HW) * d.value_hidden_size + d.value_hidden_size + (size_t)d.value_hidden_size * d.num_values +
+    if (d.concat_all_layers) n += (size_t)cal_layers(d) * (F + cb + 4);   // a conv + BN per trunk layer
+    else n += F + cb + (d.value_bn ? 4 : 0);
+    n += (size_t)value_features(d) * d.value_hidden_size + d.value_hidden_size + (size_t)d.value_hidden_size * d.num_values +
          d.num_values;
     return n;
 }
@@ -138,6 +147,10 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     if (initial_kernel(d) != 1 && initial_kernel(d) != 3) { fail("initial conv kernel must be 1 or 3"); return nullptr; }
     if (d.se_units < 0 || d.se_units > kMaxSE || (d.se_units && !d.resnet_v2)) {
         fail("squeeze-excite units must be 0.." + std::to_string(kMaxSE) + " on a v2 net");
+        return nullptr;
+    }
+    if (d.concat_all_layers && (!d.resnet_v2 || d.global_pooling_value || d.value_bn)) {
+        fail("concat_all_layers needs a v2 net without the pooling value head (model.py:251-252)");
         return nullptr;
     }
     const int precision = d.precision == 0 ? GZ_PRECISION_BF16 : d.precision;
@@ -201,7 +214,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         t.nb = c.nb;
         t.threads = c.threads;
         t.name = c.name;
-        t.fused_heads = !c.single_image;
+        t.fused_heads = !c.single_image && !d.concat_all_layers;
         const int scr = t.fused_heads ? std::max(scr_in, fused_heads_bytes(npos, d.role_count, maxP, d.value_hidden_size,
                                                                            gap_features(d), c.nb))
                                       : scr_in;
@@ -211,11 +224,14 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         t.smem = t.btab_off + bias_table_bytes(fpad, d.residual_layers);
         t.se_off = t.smem;
         if (d.se_units) t.smem += se_scratch_bytes(fpad, c.nb);
+        t.cal_off = t.smem;
+        if (d.concat_all_layers) t.smem += align16(4 * c.nb * npos * 4);
         return t;
     };
     net->small = trunk(kc);
     net->large = trunk(kl);
-    net->heads_smem = heads_lds_bytes(npos, d.role_count, maxP, d.value_hidden_size, gap_features(d));
+    const int FS = 2 * d.role_count * npos + value_features(d);   // head features per board
+    net->heads_smem = heads_lds_bytes(FS, maxP, d.value_hidden_size);
     // Large policies on nets whose every launch runs the separate heads kernel: the policy Dense
     // layers run as one MFMA GEMM per launch (policy_gemm_kernel) instead of heads_kernel's
     // per-4-board fp32 loop (amazons P = 3041: 12 % of the forward).  Every launch of such a net
@@ -237,7 +253,10 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     kp.init_act = has_initial_bn(d) ? 1 : 0;
     kp.S = d.se_units;
     kp.gapF = gap_features(d);
-    kp.FS = (2 * d.role_count + 1) * npos + kp.gapF;
+    kp.FS = FS;
+    kp.VK = value_features(d);
+    kp.cal = cal_layers(d);
+    kp.nofuse = d.concat_all_layers ? 1 : 0;
     kp.maxP = maxP;
     kp.npos = npos;
     kp.gemm_heads = net->gemm_heads ? 1 : 0;
@@ -304,7 +323,8 @@ extern "C" double gz_net_flops_per_eval(const gz_net* net) {
     double f = 2 * HW * C * F * k0 * k0 + d.residual_layers * 2 * (2 * HW * F * F * 9);
     f += d.residual_layers * 2.0 * (2 * F * d.se_units);
     for (int r = 0; r < d.role_count; ++r) f += 2 * HW * F * 2 + 2 * (2 * HW) * d.policy_dist_count[r];
-    f += 2 * HW * F + 2 * (gap_features(d) + HW) * d.value_hidden_size + 2.0 * d.value_hidden_size * d.num_values;
+    f += 2 * HW * F * std::max(1, cal_layers(d)) + 2.0 * value_features(d) * d.value_hidden_size +
+         2.0 * d.value_hidden_size * d.num_values;
     return f;
 }
 
@@ -331,7 +351,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     const int F = d.cnn_filter_size, C = d.input_channels, B = d.residual_layers, R = d.role_count;
     const int FP = net->fpad;
     const int HW = d.input_columns * d.input_rows, K0 = net->K0, KC = FP / 32;
-    const int HC = 2 * R + 1;
+    const int HC = 2 * R + 1;      // head 1x1 convs (the value conv: unused with concat_all_layers)
+    const int NL = cal_layers(d);
     const float eps = 1e-3f;
 
     // host images
@@ -349,6 +370,7 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     };
     std::vector<float> bres((size_t)2 * B * FP, 0.f);
     std::vector<float> wh((size_t)HC * FP, 0.f), bh(HC, 0.f);
+    std::vector<float> wcl((size_t)std::max(NL, 1) * FP, 0.f), bcl(std::max(NL, 1), 0.f);
 
     Cursor cur{blob};
     // BN after a conv with bias cb (legacy model files): gamma*(conv + cb - mean)/sqrt(var+eps) + beta
@@ -452,7 +474,14 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
         pdense[r] = cur.take((size_t)2 * HW * d.policy_dist_count[r]);
         pbias[r] = cur.take(d.policy_dist_count[r]);
     }
-    {
+    for (int j = 0; j < NL; ++j) {   // concat_all_layers: conv2d_block(1, 1) per trunk layer, BN folded
+        const float* w = cur.take(F);
+        const float* cb = conv_bias(1);
+        bn_fold(1, s, bb, cb);
+        for (int f = 0; f < F; ++f) wcl[(size_t)j * FP + f] = w[f] * s[0];
+        bcl[j] = bb[0];
+    }
+    if (NL == 0) {
         const float* w = cur.take(F);   // [1][1][F][1], no BN, no bias (model.py:275-279)
         const float* cb = conv_bias(1);  // legacy files: bias, then BN (value_bn)
         float vs = 1.f, vb = cb ? cb[0] : 0.f;
@@ -464,7 +493,7 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
         for (int f = 0; f < F; ++f) wh[(size_t)(2 * R) * FP + f] = w[f] * vs;
         bh[2 * R] = vb;
     }
-    const int VK = gap_features(d) + HW;     // value hidden inputs: [GAP F] + HW
+    const int VK = value_features(d);       // value hidden inputs: [GAP F] + HW, or (B + 1) HW
     const float* vhw = cur.take((size_t)VK * d.value_hidden_size);
     const float* vhb = cur.take(d.value_hidden_size);
     const float* vdw = cur.take((size_t)d.value_hidden_size * d.num_values);
@@ -477,6 +506,7 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     const size_t o_b0 = L.alloc(b0.size() * 4);
     const size_t o_wres = L.alloc(wres.size() * 2), o_bres = L.alloc(bres.size() * 4);
     const size_t o_wh = L.alloc(wh.size() * 4), o_bh = L.alloc(bh.size() * 4);
+    const size_t o_wcl = L.alloc(wcl.size() * 4), o_bcl = L.alloc(bcl.size() * 4);
     size_t o_pd[GZ_MAX_ROLES], o_pb[GZ_MAX_ROLES];
     for (int r = 0; r < R; ++r) {
         o_pd[r] = L.alloc((size_t)2 * HW * d.policy_dist_count[r] * 4);
@@ -518,6 +548,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     put(o_bres, bres.data(), bres.size() * 4);
     put(o_wh, wh.data(), wh.size() * 4);
     put(o_bh, bh.data(), bh.size() * 4);
+    put(o_wcl, wcl.data(), wcl.size() * 4);
+    put(o_bcl, bcl.data(), bcl.size() * 4);
     for (int r = 0; r < R; ++r) {
         // Keras layout [2HW][P_r] (k-major): heads_kernel reads one k row coalesced across outputs
         put(o_pd[r], pdense[r], (size_t)2 * HW * d.policy_dist_count[r] * 4);
@@ -553,6 +585,8 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     kp.bres = (const float*)(m + o_bres);
     kp.wh = (const float*)(m + o_wh);
     kp.bh = (const float*)(m + o_bh);
+    kp.wcl = (const float*)(m + o_wcl);
+    kp.bcl = (const float*)(m + o_bcl);
     for (int r = 0; r < R; ++r) {
         kp.pd[r] = (const float*)(m + o_pd[r]);
         kp.pb[r] = (const float*)(m + o_pb[r]);
@@ -654,6 +688,7 @@ static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* se
     }
     kp.btab_off = t.btab_off;
     kp.se_off = t.se_off;
+    kp.cal_off = t.cal_off;
     void* args[] = {&kp};
     HIPCHK(hipLaunchKernel(t.fn, dim3((n + t.nb - 1) / t.nb), dim3(t.threads), args, t.smem, stream));
     if (mid) HIPCHK(hipEventRecord(mid, stream));

@@ -17,8 +17,10 @@ optional ``ResLayer_<i>_se_compress / se_gating`` squeeze-excite Dense layers, a
 (bare in older files, ``initial-conv_conv2d / _bn`` in current ones) and the global-pooling value head
 (``value_average`` + ``value_flatten_conv2d`` [+ ``_bn``], concatenated GAP-first, ``model.py:262-271``).
 Files built by older model.py revisions with layers the current one cannot produce
-(AveragePooling2D / Lambda reward heads, e.g. ``hexLG13/models/h1_229.json``) and the
-``concat_all_layers`` value head raise :class:`NotSupported`.
+(AveragePooling2D / Lambda reward heads, e.g. ``hexLG13/models/h1_229.json``) raise
+:class:`NotSupported`.  The ``concat_all_layers`` value head (``model.py:251-260``: one
+``value_flatten_<j>_conv2d`` + ``_bn`` per trunk layer, flattened and concatenated in layer order, e.g.
+``hex19/models/h2_477.json``) maps to ``concat_all_layers``.
 
 ``weights_from_keras`` maps per-layer Keras weight lists (``layer.get_weights()``: Conv2D
 ``[kernel HWIO, bias?]``, BatchNormalization ``[gamma, beta, moving_mean, moving_variance]``, Dense
@@ -53,11 +55,11 @@ def _inbound(layer):
 
 
 def _is_conv(role):
-    return re.match(r"(initial_conv|res\d+_conv[012]|policy\d+_conv|value_conv)$", role) is not None
+    return re.match(r"(initial_conv|res\d+_conv[012]|policy\d+_conv|value\d*_conv)$", role) is not None
 
 
 def _is_bn(role):
-    return re.match(r"(initial_bn|res\d+_bn[012]|policy\d+_bn|value_bn)$", role) is not None
+    return re.match(r"(initial_bn|res\d+_bn[012]|policy\d+_bn|value\d*_bn)$", role) is not None
 
 
 def _is_se(role):
@@ -83,6 +85,8 @@ def roles(doc):
                 out[n] = "initial_conv"
             elif re.search(r"policy_head_(\d+)", n):
                 out[n] = "policy%s_conv" % re.search(r"policy_head_(\d+)", n).group(1)
+            elif re.match(r"value_flatten_(\d+)_conv2d$", n):   # concat_all_layers, model.py:255-257
+                out[n] = "value%s_conv" % re.match(r"value_flatten_(\d+)_conv2d$", n).group(1)
             elif "value" in n:
                 out[n] = "value_conv"
             else:
@@ -171,6 +175,7 @@ def desc_from_keras_json(doc):
         raise NotSupported("squeeze-excite on some blocks only")
     # global-pooling value head (model.py:262-271): Concatenate([GAP(trunk), flatten(value conv)])
     gap = False
+    concat = False
     for n in cfg:
         if cls[n] == "GlobalAveragePooling2D" and not n.startswith("ResLayer_"):
             gap = True
@@ -181,10 +186,28 @@ def desc_from_keras_json(doc):
                 while cls[x] in ("Flatten", "Reshape", "Activation", "BatchNormalization", "Dropout"):
                     x = _inbound(by_name[x])[0]
                 return cls[x]
-            if [origin(x) for x in srcs] != ["GlobalAveragePooling2D", "Conv2D"]:
-                raise NotSupported("concatenated value head %s (only the GAP-first pooling head)" % n)
-    if v2 and not gap and any(cls[n] == "Concatenate" for n in cfg):
-        raise NotSupported("concat_all_layers value head")
+            origins = [origin(x) for x in srcs]
+            if origins == ["GlobalAveragePooling2D", "Conv2D"]:
+                continue
+            if not v2 or set(origins) != {"Conv2D"}:
+                raise NotSupported("concatenated value head %s" % n)
+            # concat_all_layers (model.py:251-260): value conv j reads trunk layer j -- the initial
+            # conv block's output, then each residual block's add -- in concatenation order
+
+            def conv_of(x):
+                while cls[x] != "Conv2D":
+                    x = _inbound(by_name[x])[0]
+                return x
+            convs = [conv_of(x) for x in srcs]
+            if [r.get(c) for c in convs] != ["value%d_conv" % j for j in range(len(blocks) + 1)]:
+                raise NotSupported("concat_all_layers value convs out of layer order")
+            for j, c in enumerate(convs):
+                src = _inbound(by_name[c])[0]
+                want = (lambda x: x.startswith("initial-conv") or r.get(x) == "initial_conv") if j == 0 else \
+                    (lambda x, j=j: x == "ResLayer_%d_add" % (j - 1))
+                if not want(src):
+                    raise NotSupported("concat_all_layers value conv %d reads %s" % (j, src))
+            concat = True
     flat = [c for n, c in cfg.items() if cls[n] == "Flatten"]
     dfs = {c.get("data_format") for c in flat}
     if len(dfs) != 1:
@@ -200,7 +223,8 @@ def desc_from_keras_json(doc):
                    cnn_kernel_size=k, leaky_relu=leaky, flatten_nchw=flatten_nchw, conv_bias=conv_bias.pop(),
                    value_bn="value_bn" in r.values(), value_sigmoid=vact == "sigmoid",
                    resnet_v2=v2, initial_bn="initial_bn" in r.values(), se_units=se.pop() if se else 0,
-                   global_pooling_value=gap, initial_kernel_size=0 if k0 == default_k0 else k0)
+                   global_pooling_value=gap, initial_kernel_size=0 if k0 == default_k0 else k0,
+                   concat_all_layers=concat)
 
 
 def weights_from_keras(doc, layer_weights):

@@ -13,8 +13,8 @@ def desc_from_conf(nn_model_conf, generation_descr=None):
     (model.py:154-296): v1, or v2 with squeeze-excite (ratio 3, :190-197) and the global-pooling
     value head (whose 1x1 conv has BN, :265-268)."""
     c = nn_model_conf
-    if c.concat_all_layers:
-        raise NotImplementedError("concat_all_layers value head (model.py:251-260) has no HIP forward")
+    if c.concat_all_layers and (not c.resnet_v2 or c.global_pooling_value):
+        raise ValueError("concat_all_layers needs resnet_v2 and no global_pooling_value (model.py:170-252)")
     if c.squeeze_excite_layers and not c.resnet_v2:
         raise ValueError("squeeze_excite_layers needs resnet_v2 (model.py:202)")
     se = c.cnn_filter_size // 3 if (c.resnet_v2 and c.squeeze_excite_layers) else 0
@@ -26,7 +26,7 @@ def desc_from_conf(nn_model_conf, generation_descr=None):
                    policy_dist_count=list(c.policy_dist_count), value_hidden_size=c.value_hidden_size,
                    num_values=3 if draw else 2, cnn_kernel_size=c.cnn_kernel_size, leaky_relu=c.leaky_relu,
                    resnet_v2=bool(c.resnet_v2), se_units=se, global_pooling_value=bool(c.global_pooling_value),
-                   value_bn=bool(c.global_pooling_value))
+                   value_bn=bool(c.global_pooling_value), concat_all_layers=bool(c.concat_all_layers))
 
 
 class HipModel(object):

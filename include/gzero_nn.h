@@ -57,6 +57,10 @@ typedef struct gz_net_desc {
     int initial_bn;                           /* v2: BN + act after the initial conv (0: bare conv)  */
     int se_units;                             /* squeeze-excite compress units, 0 = none (<= 64)     */
     int global_pooling_value;                 /* value features = [trunk channel means (F), conv (HW)] */
+    /* v2 only, model.py:251-260: the value head reads every trunk layer (the initial conv block's
+     * output and each residual block's add), each through its own 1x1 conv + BN + act: (B + 1) HW
+     * features in layer order.  Such nets run the dense heads in a separate heads launch. */
+    int concat_all_layers;
 } gz_net_desc;
 
 #define GZ_PRECISION_BF16 1

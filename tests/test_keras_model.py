@@ -22,7 +22,7 @@ V1_FILES = {"amazons_10x10/models/h1_27.json", "breakthrough/models/x6_102.json"
 V2_FILES = {"amazons_10x10/models/f1_105.json", "breakthrough/models/f1_396.json",
             "breakthroughSmall/models/b1_58.json", "chess/models/c2_260.json", "chess/models/kb1_283.json",
             "draughts_killer/models/f1_581.json", "hexLG11/models/b1_173.json", "hexLG13/models/b4_305.json",
-            "hexLG13/models/d2_194.json", "reversi_8x8/models/f2_308.json"}
+            "hexLG13/models/d2_194.json", "reversi_8x8/models/f2_308.json", "hex19/models/h2_477.json"}
 
 @pytest.fixture(scope="module")
 def golden():
@@ -47,7 +47,10 @@ def test_golden_files(golden):
     rejected = {k: v["not_supported"] for k, v in golden.items() if "not_supported" in v}
     assert "AveragePooling2D" in rejected["hexLG13/models/h1_229.json"]
     assert "Lambda" in rejected["breakthrough/models/kt1_206.json"]
-    assert "concatenated value head" in rejected["hex19/models/h2_477.json"]     # concat_all_layers
+    c = ok["hex19/models/h2_477.json"]             # v2 concat_all_layers value head (model.py:251-260)
+    assert c.concat_all_layers and not c.global_pooling_value and c.value_features == (10 + 1) * 19 * 19
+    assert all(k in rejected for k in golden if k not in ok) and len(rejected) == 8
+    assert all(("AveragePooling2D" in v or "Lambda" in v) for v in rejected.values())
     assert len(rejected) + len(ok) == len(golden)
 
 
@@ -152,7 +155,8 @@ def _random_layer_weights(shapes, seed):
 
 @pytest.mark.parametrize("key", ["breakthrough/models/x6_102.json", "breakthroughSmall/models/b1_58.json",
                                  "breakthrough/models/f1_396.json", "hexLG13/models/b4_305.json",
-                                 "draughts_killer/models/f1_581.json", "reversi_8x8/models/f2_308.json"])
+                                 "draughts_killer/models/f1_581.json", "reversi_8x8/models/f2_308.json",
+                                 "hex19/models/h2_477.json"])   # concat_all_layers value head
 def test_weight_mapping(golden, key):
     g = golden[key]
     desc = NetDesc(**g["desc"])

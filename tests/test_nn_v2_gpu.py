@@ -31,7 +31,9 @@ TOL_FP32_KL = 4e-7               # max over rows of KL(oracle || kernel)
 RES_GAMMA = 0.3                  # damps the v2 stream's growth so the softmaxes stay in the interior
 
 with open(os.path.join(os.path.dirname(__file__), "golden", "keras_descs.json")) as _f:
-    FILES = {k: NetDesc(**v["desc"]) for k, v in json.load(_f).items() if "desc" in v and v["desc"]["resnet_v2"]}
+    _ALL = {k: NetDesc(**v["desc"]) for k, v in json.load(_f).items() if "desc" in v and v["desc"]["resnet_v2"]}
+# the kernels hold boards of up to 13 x 13 (176 positions): hex19 (19 x 19, h2_477) is outside them
+FILES = {k: d for k, d in _ALL.items() if d.hw <= 169}
 
 
 def _err(a, b):
@@ -159,3 +161,43 @@ def test_v2_keras_dropin(game, key, hip_device):
         er = _err(a, b)
         print("v2 keras drop-in %s out%d max %.3g mean %.3g" % (key, i, er[0], er[1]))
         assert er[0] <= TOL_V2_BF16[0] and er[1] <= TOL_V2_BF16[1]
+
+
+# concat_all_layers value head (model.py:251-260; the reference's hex19/models/h2_477.json: F = 80,
+# 10 blocks, SE 26, 19 x 19) on synthetic v2 nets the kernels hold: 8 x 8 (two-board kernels, split
+# and bf16) and 13 x 13 (single-image kernel, bf16), with and without squeeze-excite.
+CONCAT_NETS = {
+    "concat_8x8_se": NetDesc(5, 8, 8, 128, 6, [155, 155], resnet_v2=True, se_units=42, concat_all_layers=True),
+    "concat_8x8_f80": NetDesc(5, 8, 8, 80, 3, [155, 155], value_hidden_size=128, resnet_v2=True, se_units=26,
+                              concat_all_layers=True, flatten_nchw=True),
+    "concat_13x13": NetDesc(5, 13, 13, 80, 4, [170, 171], value_hidden_size=128, resnet_v2=True, se_units=26,
+                            concat_all_layers=True),
+    "concat_13x13_nose": NetDesc(5, 13, 13, 64, 3, [170, 171], resnet_v2=True, concat_all_layers=True),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CONCAT_NETS))
+def test_v2_concat_all_layers(name, hip_device):
+    """The per-layer value convs run inside the trunk (each layer's features from the fp32 stream),
+    the dense heads in heads_kernel; one- and two-board launches (1 and 300 rows)."""
+    desc = CONCAT_NETS[name]
+    w = random_weights(desc, 7919, bias_std=0.2, res_gamma=RES_GAMMA)
+    for n in (1, 300):
+        x = random_planes(desc, n, 100 + n)
+        _check(name, desc, w, x, hip_device, "bf16", TOL_V2_BF16)
+        if desc.hw <= 64:
+            _check(name, desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
+
+
+def test_v2_concat_all_layers_batch_invariance(hip_device):
+    from galvanise_zero_amd._native import HipNet
+    desc = CONCAT_NETS["concat_8x8_se"]
+    for precision in ("bf16", "fp32"):
+        net = HipNet(desc, hip_device, precision)
+        net.set_weights(to_blob(random_weights(desc, 3, bias_std=0.2, res_gamma=RES_GAMMA)))
+        x = random_planes(desc, 300, 9)
+        full = net.forward(x)
+        perm = np.random.default_rng(0).permutation(300)[:37]
+        for a, b in zip(full, net.forward(x[perm])):
+            assert np.array_equal(a[perm], b)
+        net.close()

@@ -7,6 +7,7 @@ TAG=${1:-r04a}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 T=$R/gpurun_out/$TAG
 mkdir -p $T
+timeout -k 10 300 python -u -m pytest tests/test_nn_v2_gpu.py -k concat -x -v --timeout 120 --timeout-method thread > $T/concat_tests.log 2>&1; echo "concat tests rc=$?"; tail -1 $T/concat_tests.log
 timeout -k 10 500 python -u tools/split_error_dist.py $T/split_error_dist.json --seeds 10 > $T/split_error_dist.log 2>&1 || { echo "error dist failed"; tail -20 $T/split_error_dist.log; exit 1; }
 grep "max over" $T/split_error_dist.log
 bash tools/gpu_pmc_r04.sh $TAG/pmc > $T/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $T/pmc.log; exit 1; }
