@@ -113,13 +113,28 @@ void* node_alloc(size_t bytes) {   // bytes: a multiple of 64
         unpoison(p, bytes);
         return p;
     }
-    {   // blocks of exited threads / destroyed pools
+    {   // blocks of exited threads / destroyed pools: take up to kRefill at once (one lock per
+        // batch, not per node, when a new runner's threads draw on a destroyed one's trees)
+        constexpr int kRefill = 64;
         NodePool& pool = node_pool();
-        std::lock_guard<std::mutex> lk(pool.mu);
-        if (void* p = pool.head[c]) {
-            pool.head[c] = link_of(p);
-            unpoison(p, bytes);
-            return p;
+        void* first = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(pool.mu);
+            first = pool.head[c];
+            if (first != nullptr) {
+                void* last = first;
+                int k = 1;
+                for (void* n = link_of(last); n != nullptr && k < kRefill; n = link_of(last), ++k) last = n;
+                pool.head[c] = link_of(last);
+                set_link(last, nullptr);
+            }
+        }
+        if (first != nullptr) {
+            void* rest = link_of(first);
+            for (void* q = rest; q != nullptr; q = link_of(q)) nc.blocks++;
+            nc.head[c] = rest;
+            unpoison(first, bytes);
+            return first;
         }
     }
     return nc.fresh(bytes);

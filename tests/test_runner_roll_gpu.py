@@ -97,3 +97,74 @@ def test_generation_roll_live_runner(per_pool, hip_device):
     exp = [sample_key(setup, _suffix(s), False) for s in man.samples[:n]]
     assert got == exp
     print("pool %d: %d samples identical to the oracle across the roll at batch %d" % (pool, n, k))
+
+
+@pytest.mark.timeout(300)
+def test_roll_timeout_withdraws_and_next_roll_succeeds(hip_device):
+    """A roll whose wait times out is withdrawn before gz_runner_update_network returns (the caller
+    may free its blob at once), or -- when the launcher had already claimed it -- waited for; either
+    way the runner keeps playing and the next roll succeeds (no dangling pending roll)."""
+    from galvanise_zero_amd._native import HipNet
+    from galvanise_zero_amd.runner import SelfPlayRunner
+    desc = BASELINE_CONFIGS[2]["desc"]
+    setup = Setup("breakthrough")
+    wa, wb = to_blob(random_weights(desc, 7921)), to_blob(random_weights(desc, 7922))
+    net = HipNet(desc, hip_device, "fp32")
+    net.set_weights(wa)
+    conf = templates.selfplay_config_template()
+    conf.evals_per_move = 8
+    r = SelfPlayRunner(net, setup.sm, setup.transformer, conf, device=hip_device, num_threads=2, pools_per_thread=2,
+                       batch_size=32, seed=3, spin_yield_playouts=1000, min_launch_rows=64, max_launch_wait_us=2000)
+    r.start()
+    r.wait_rows(128 * 50, timeout_s=120)
+    outcomes = []
+    for _ in range(5):
+        blob = wb.copy()
+        try:
+            r.update_network(blob, clear_unique_states=False, timeout_s=1e-7)
+            outcomes.append("applied")
+        except RuntimeError as e:
+            assert "(-2)" in str(e), e
+            outcomes.append("withdrawn")
+        del blob                    # freed right after the call returned
+        r.wait_rows(r.stats()["rows"] + 128 * 5, timeout_s=60)
+    roll = r.update_network(wa, clear_unique_states=False, timeout_s=60)
+    r.wait_rows(r.stats()["rows"] + 128 * 20, timeout_s=60)
+    r.stop()
+    r.close()
+    print("short-timeout rolls:", outcomes, "final roll", roll)
+    assert roll["launches_before"] > 0
+
+
+@pytest.mark.timeout(400)
+def test_runner_recreate_reuses_node_memory(hip_device):
+    """Trees freed by gz_runner_destroy on the caller's thread go back to the process-wide node pool
+    (node_cache_flush), so a second runner's games reuse them: the second create / play / destroy
+    cycle adds far less resident memory than the first."""
+    from galvanise_zero_amd._native import HipNet
+    from galvanise_zero_amd.runner import SelfPlayRunner
+    import bench
+
+    def rss_gb():
+        with open("/proc/self/statm") as f:
+            return int(f.read().split()[1]) * 4096 / 1e9
+
+    sm, t, desc = bench.setup_game(2)
+    net = HipNet(desc, hip_device, "fp32")
+    net.set_weights(to_blob(random_weights(desc, 7921)))
+    grow = []
+    for cycle in range(2):
+        before = rss_gb()
+        r = SelfPlayRunner(net, sm, t, bench.selfplay_conf("template", 800), device=hip_device, num_threads=8,
+                           pools_per_thread=2, batch_size=64, seed=11, spin_yield_playouts=1000,
+                           min_launch_rows=1024, max_launch_wait_us=3000)
+        r.start()
+        r.wait_rows(2_000_000, timeout_s=150)
+        r.stop()
+        peak = rss_gb()
+        r.close()
+        grow.append(peak - before)
+        print("cycle %d: rss %.2f -> %.2f GB (+%.2f), after destroy %.2f GB" % (cycle, before, peak, peak - before,
+                                                                                rss_gb()))
+    assert grow[0] > 0.3, grow                 # the first cycle built real trees
+    assert grow[1] < 0.5 * grow[0], grow       # the second reused the freed blocks
