@@ -1329,6 +1329,8 @@ trunk_kernel_v2(const KParams kp) {
 // the same operations for every BPW, so outputs do not depend on how boards are grouped (fused into
 // the trunk kernel with BPW = its NB, or in heads_kernel with BPW = 4).  Every thread of the
 // workgroup (4 waves) must call it; boards board0 .. board0 + nb - 1 are written.
+constexpr int kGemmSoftmaxMax = 3072;   // policy rows the register softmax of gemm_heads takes (48 per lane)
+
 template <int BPW, int NT>
 __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, float* lg, int board0, int nb) {
     static_assert(BPW >= 1 && BPW <= 4, "one softmax wave per board");
@@ -1343,7 +1345,37 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
         const float* fr = fk + (size_t)r * 2 * NPOS * BPW;
         int lof = 0;
         for (int q = 0; q < r; ++q) lof += kp.P[q];
-        if (kp.gemm_heads) {   // logits computed by policy_gemm_kernel (bias included)
+        if (kp.gemm_heads && P <= kGemmSoftmaxMax) {
+            // logits computed by policy_gemm_kernel (bias included): wave b takes board b's row
+            // straight from the logits scratch into registers -- every load of the row in flight at
+            // once instead of a load / LDS-store round trip per 256 values -- with the same
+            // per-lane order (j = lane, lane + 64, ...) and reductions as the LDS path below
+            if (wave < nb) {
+                constexpr int NV = kGemmSoftmaxMax / 64;
+                const int b = wave, board = board0 + b;
+                const float* l = kp.glog + (size_t)board * kp.plog + lof;
+                float v[NV];
+#pragma unroll
+                for (int i = 0; i < NV; ++i) v[i] = lane + 64 * i < P ? l[lane + 64 * i] : -3.0e38f;
+                float m = -3.0e38f;
+#pragma unroll
+                for (int i = 0; i < NV; ++i) m = fmaxf(m, v[i]);
+                m = wave_max(m);
+                float sum = 0.f;
+#pragma unroll
+                for (int i = 0; i < NV; ++i)
+                    if (lane + 64 * i < P) sum += __expf(v[i] - m);
+                sum = wave_sum(sum);
+                const float inv = 1.f / sum;
+                const int sg = find_segment(kp, board);
+                float* out = kp.seg[sg].pol[r] + (size_t)(board - kp.seg[sg].row0) * P;
+#pragma unroll
+                for (int i = 0; i < NV; ++i)
+                    if (lane + 64 * i < P) out[lane + 64 * i] = kp.logits ? v[i] : __expf(v[i] - m) * inv;
+            }
+            continue;
+        }
+        if (kp.gemm_heads) {   // (rows longer than the register path) through LDS
             for (int i = tid; i < nb * P; i += NT) {
                 const int b = i / P, j = i - b * P;
                 lg[b * LMAX + j] = kp.glog[(size_t)(board0 + b) * kp.plog + lof + j];
@@ -1513,9 +1545,21 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
     const int tid = threadIdx.x;
     const int board0 = blockIdx.x * BPW;
     const int nb = kp.n - board0 < BPW ? kp.n - board0 : BPW;
-    for (int i = tid; i < BPW * FS; i += 256) {
-        const int b = i / FS, k = i - b * FS;
-        fk[k * BPW + b] = b < nb ? kp.feat[(size_t)(board0 + b) * FS + k] : 0.f;
+    // the boards' features, 8 loads per thread in flight per round (not one load / store at a time)
+    for (int i0 = 0; i0 < BPW * FS; i0 += 8 * 256) {
+        float r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 256 + tid;
+            const int b = i / FS, k = i - b * FS;
+            r[u] = (i < BPW * FS && b < nb) ? kp.feat[(size_t)(board0 + b) * FS + k] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 256 + tid;
+            const int b = i / FS, k = i - b * FS;
+            if (i < BPW * FS) fk[k * BPW + b] = r[u];
+        }
     }
     __syncthreads();
     dense_heads<BPW>(kp, fk, lg, board0, nb);

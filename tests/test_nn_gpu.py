@@ -308,6 +308,8 @@ def test_split_precision_against_fp32(hip_device):
         print("precision %-18s max |err| vs float64 oracle per output: %s" % (k, " ".join("%.3g" % e for e in v)))
     split, f32, b16 = max(errs["split"]), max(errs["fp32 (torch-CPU)"]), max(errs["bf16"])
     # measured on MI355X (profiles/r03s_gpu_tests.log): fp32 5.7e-6, split 2.0e-4, bf16 5.9e-2 (the
-    # undamped bench weights at 1,024 rows; tolerance 3x the split's)
+    # undamped bench weights at 1,024 rows); the split's bound is the stated cfg2 tolerance
+    # (galvanise_zero_amd/nn/tolerance.py: 3x the max over 10 seeds, profiles/r04a_split_error_dist.json)
+    from galvanise_zero_amd.nn.tolerance import SPLIT_TOLERANCE
     assert f32 < split < b16
-    assert split <= 6e-4 and split * 20 < b16
+    assert split <= SPLIT_TOLERANCE["cfg2"]["max"] and split * 20 < b16
