@@ -1837,6 +1837,140 @@ __attribute__((noinline)) void spin_wins(SpinRegs& x, int limit) {
     x.failed = failed;
 }
 
+// spin_wins for two roles and up to four all-win candidates, with the per-candidate arithmetic in
+// AVX2 lanes: the candidates' exploration terms are one packed float multiply (pc * P, float as in the
+// reference), one packed double multiply and ONE packed double division (vdivpd) instead of NC scalar
+// divisions, and the state stays in vector registers.  Lane k computes exactly the scalar expression
+// of candidate k (IEEE packed arithmetic, no contraction), so the choice is the same.  The root's
+// current scores are updated speculatively: deep in a spin cur = (v cur + s) / (v + 1) rounds back to
+// cur, so the update is computed from the held value and compared (bitwise) instead of chained through
+// every playout's divisions -- a changed value is taken as usual.
+template <int NC>
+__attribute__((noinline, target("avx2"))) void spin_wins_v(SpinRegs& x, int limit) {
+    static_assert(NC >= 2 && NC <= 4, "lanes");
+    alignas(32) float Pa[4] = {0.f, 0.f, 0.f, 0.f};
+    alignas(16) int32_t Ta[4] = {0, 0, 0, 0};
+    for (int k = 0; k < NC; ++k) { Pa[k] = x.P[k]; Ta[k] = (int32_t)x.T[k]; }
+    uint32_t LV[NC], T0[NC];
+    for (int k = 0; k < NC; ++k) { LV[k] = x.LV[k]; T0[k] = x.T[k]; }
+    __m128 Pv = _mm_load_ps(Pa);
+    __m128i Tv = _mm_load_si128((const __m128i*)Ta);
+    const __m128i lane_id = _mm_set_epi32(3, 2, 1, 0);
+    const __m128i one_i = _mm_set1_epi32(1);
+    const float win_base = x.BASE[0];
+    const float sc0 = x.lsc[0][0], sc1 = x.lsc[0][1];
+    float cur0 = x.cur[0], cur1 = x.cur[1];
+    const int lead = x.lead;
+    const float limit_latch_root = 0.66;
+    const float pc_root = x.pc_root;
+    const bool noise_check = x.noise_check;
+    const double ub = x.ub;
+    const uint32_t v_end = x.v_end;
+    const uint64_t reach = x.reach;
+    uint32_t v = x.v, touched = 0;
+    float pc = x.pc;
+    uint64_t discards = 0;
+    int done = 0;
+    bool failed = false;
+    PuctLogCursor plog;
+    uint32_t tmax = 0;
+    for (int k = 0; k < NC; ++k) tmax = std::max(tmax, x.T[k]);
+    const uint32_t run_max = std::min<uint32_t>((uint32_t)std::max(limit, 0), v_end - v);
+    const bool check_latch = !((double)tmax + run_max < 0.66 * (double)v * (1.0 - 1e-5));
+    alignas(32) double sa[4];
+    while (done < limit && v < v_end) {
+        const float lead_cur = lead == 0 ? cur0 : cur1;
+        if (noise_check && lead_cur <= 0.95) {
+            failed = true;
+            break;
+        }
+        pc = plog.at(v);
+        pc += pc_root;
+        const double sqrt_node_visits = sqrt_pos(v + 1);
+        const bool latch = v > 1000 && v < 40000000;
+        if (check_latch) {
+            _mm_store_si128((__m128i*)Ta, Tv);
+            bool latched_win = false;
+            for (int k = 0; k < NC; ++k) {
+                const uint32_t t = (uint32_t)Ta[k];
+                latched_win |= t > 16 && t > v * limit_latch_root;
+            }
+            if (latch && latched_win) {
+                failed = true;
+                break;
+            }
+        }
+        double child_score = win_base;
+        child_score *= 1.0f + pc;
+        // exploration_score = pc * P[k] * sqrt_node_visits / (traversals + 0.0), traversals = T[k] + 1
+        const __m128 pcP = _mm_mul_ps(_mm_set1_ps(pc), Pv);
+        const __m256d num = _mm256_mul_pd(_mm256_cvtps_pd(pcP), _mm256_set1_pd(sqrt_node_visits));
+        const __m256d den = _mm256_add_pd(_mm256_cvtepi32_pd(_mm_add_epi32(Tv, one_i)), _mm256_setzero_pd());
+        const __m256d score = _mm256_add_pd(_mm256_set1_pd(child_score), _mm256_div_pd(num, den));
+        _mm256_store_pd(sa, score);
+        float best_score = -1;
+        int best = -1;
+        double best_exact = 0.0;
+        for (int k = 0; k < NC; ++k) {
+            if (sa[k] > best_score) {
+                best = k;
+                best_score = sa[k];
+                best_exact = sa[k];
+            }
+        }
+        if (best < 0 || !(ub < best_exact) || !(ub <= (double)(float)best_exact)) {
+            failed = true;
+            break;
+        }
+        discards += latch ? reach : 0;
+        touched |= 1u << best;
+        {
+            float visits = v;
+            if (visits > 100000) visits = 100000 + 0.1f * (visits - 100000);
+            const float n0 = ((visits * cur0 + sc0) / (visits + 1.0f));
+            const float n1 = ((visits * cur1 + sc1) / (visits + 1.0f));
+            // (bitwise: the update is taken whenever it changes a bit)
+            if (__builtin_expect(__builtin_bit_cast(uint32_t, n0) != __builtin_bit_cast(uint32_t, cur0), 0)) cur0 = n0;
+            if (__builtin_expect(__builtin_bit_cast(uint32_t, n1) != __builtin_bit_cast(uint32_t, cur1), 0)) cur1 = n1;
+        }
+        v++;
+        const __m128i sel = _mm_cmpeq_epi32(lane_id, _mm_set1_epi32(best));
+        Tv = _mm_sub_epi32(Tv, sel);                     // T[best] += 1 (sel lanes are -1)
+        if (v > 23) {
+            float apply = 1.0f, minimum = 0.0f;
+            decay_params(lead == 0 ? cur0 : cur1, &apply, &minimum);
+            // P[best] = max(minimum, P[best] * apply) when P[best] > minimum (std::max(a, b): b if a < b)
+            const __m128 mn = _mm_set1_ps(minimum);
+            const __m128 pn = _mm_mul_ps(Pv, _mm_set1_ps(apply));
+            const __m128 clamped = _mm_blendv_ps(mn, pn, _mm_cmplt_ps(mn, pn));
+            const __m128 upd = _mm_and_ps(_mm_castsi128_ps(sel), _mm_cmpgt_ps(Pv, mn));
+            Pv = _mm_blendv_ps(Pv, clamped, upd);
+        }
+        ++done;
+        if (v % 100 == 0) {
+            _mm_store_ps(Pa, Pv);
+            spin_normalise(x, Pa, NC);
+            Pv = _mm_load_ps(Pa);
+            if (x.expired) break;
+        }
+    }
+    _mm_store_ps(Pa, Pv);
+    _mm_store_si128((__m128i*)Ta, Tv);
+    for (int k = 0; k < NC; ++k) {
+        x.P[k] = Pa[k];
+        x.T[k] = (uint32_t)Ta[k];
+        x.LV[k] = LV[k] + ((uint32_t)Ta[k] - T0[k]);   // the win's visits rise with its traversals
+    }
+    x.cur[0] = cur0;
+    x.cur[1] = cur1;
+    x.v = v;
+    x.pc = pc;
+    x.discards += discards;
+    x.touched |= touched;
+    x.done += done;
+    x.failed = failed;
+}
+
 // any candidate mix (wins and watched scored children)
 void spin_mixed(SpinRegs& x, int limit) {
     const float limit_latch_root = 0.66;
@@ -1945,9 +2079,14 @@ int PuctEvaluator::spinRunRegs(int limit) {
     x.node = node;
     x.cand = spin.cand;
     x.drift = spin.drift;
-    if (all_win && x.role_count == 2 && nc == 2) spin_wins<2, 2>(x, limit);
-    else if (all_win && x.role_count == 2 && nc == 3) spin_wins<3, 2>(x, limit);
-    else if (all_win && x.role_count == 2 && nc == 4) spin_wins<4, 2>(x, limit);
+    // GZ_SPIN_VEC=1: the AVX2 register loops (A/B; both compute the same playouts)
+    static const bool vec = [] {
+        const char* e = std::getenv("GZ_SPIN_VEC");
+        return e != nullptr && e[0] == '1';
+    }();
+    if (all_win && x.role_count == 2 && nc == 2) vec ? spin_wins_v<2>(x, limit) : spin_wins<2, 2>(x, limit);
+    else if (all_win && x.role_count == 2 && nc == 3) vec ? spin_wins_v<3>(x, limit) : spin_wins<3, 2>(x, limit);
+    else if (all_win && x.role_count == 2 && nc == 4) vec ? spin_wins_v<4>(x, limit) : spin_wins<4, 2>(x, limit);
     else spin_mixed(x, limit);
     const int done = x.done;
     // write back (a selection that failed still ran setPuctConstant)
