@@ -65,11 +65,14 @@ PMC_PER_LAUNCH = {"gznn::trunk_kernel<128, 4, 2, 1, 3>": {
               "1024-row launches, tools/gpu_pmc_r04.sh): busy cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)"}}
 
 
-def per_game_cost(o, threads):
+def per_game_cost(o, threads, slots):
     """Per-game cost by the game's ordinal within its slot (gz_ordinal_stats of rank 0's runner, the
-    whole run): is a slot's k-th game dearer than its first?  Plus the renewal-reward estimate of the
-    stationary rate: leaf evaluations per engine-second over the completed games, times the engine
-    threads (a lower bound's complement: long games still in flight are under-represented)."""
+    whole run): is a slot's k-th game dearer than its first?  Plus the first-game cohort (ordinal 1:
+    one game per slot, every game an independent draw from the initial position with its own RNG
+    streams): its completed games' costs and the partial costs of the ones still in progress bound
+    the stationary per-game cost from below.  The completed games alone are biased towards cheap
+    games (the long spins are the ones still running), so `completed_games_evals_per_engine_s`
+    overstates the stationary rate."""
     rows = []
     for k in range(len(o["games"])):
         g = o["games"][k]
@@ -80,16 +83,23 @@ def per_game_cost(o, threads):
                      "nn_free_playouts_per_game": (o["tree_playouts"][k] - o["evals"][k]) / g,
                      "moves_per_game": o["moves"][k] / g, "spin_epochs_per_game": o["spin_epochs"][k] / g,
                      "engine_ms_per_game": 1e3 * o["engine_s"][k] / g,
-                     "evals_per_engine_s": o["evals"][k] / o["engine_s"][k] if o["engine_s"][k] > 0 else None})
+                     "evals_per_engine_s": o["evals"][k] / o["engine_s"][k] if o["engine_s"][k] > 0 else None,
+                     "in_progress": o["inflight_games_ord"][k]})
     ev, es = sum(o["evals"]), sum(o["engine_s"])
     hist = {"<%d ms" % (1 << k): c for k, c in enumerate(o["cost_hist"]) if c}
-    return {"by_ordinal": rows, "engine_ms_histogram": hist,
+    c_s = o["engine_s"][0] + o["inflight_engine_s_ord"][0]
+    c_e = o["evals"][0] + o["inflight_evals_ord"][0]
+    cohort = {"slots": slots, "completed": o["games"][0], "in_progress": o["inflight_games_ord"][0],
+              "engine_s_completed": o["engine_s"][0], "engine_s_in_progress": o["inflight_engine_s_ord"][0],
+              "evals_completed": o["evals"][0], "evals_in_progress": o["inflight_evals_ord"][0],
+              "mean_engine_ms_per_game_lower_bound": 1e3 * c_s / slots if slots else None,
+              "evals_per_engine_s_so_far": c_e / c_s if c_s > 0 else None}
+    return {"by_ordinal": rows, "engine_ms_histogram": hist, "first_game_cohort": cohort,
             "completed_games_evals_per_engine_s": ev / es if es > 0 else None,
-            "stationary_estimate_leaf_evals_per_s": threads * ev / es if es > 0 else None,
-            "in_flight": {"games": o["inflight_games"], "engine_s": o["inflight_engine_s"],
-                          "evals": o["inflight_evals"],
-                          "evals_per_engine_s": o["inflight_evals"] / o["inflight_engine_s"]
-                          if o["inflight_engine_s"] > 0 else None}}
+            "in_progress": {"games": o["inflight_games"], "engine_s": o["inflight_engine_s"],
+                            "evals": o["inflight_evals"],
+                            "evals_per_engine_s": o["inflight_evals"] / o["inflight_engine_s"]
+                            if o["inflight_engine_s"] > 0 else None}}
 
 
 def parse():
@@ -550,7 +560,7 @@ def main():
                 gbps = out["roofline"]["traffic"] / (per_variant[dom]["avg_kernel_ms"] / 1e3) / 1e9
                 out["roofline"].update({"mfma_busy_frac": busy, "hbm_GBps": gbps, "hbm_peak_GBps": PEAK_HBM_GBPS,
                                         "hbm_frac": gbps / PEAK_HBM_GBPS, "pmc_source": pmc["source"]})
-        out["per_game_cost"] = per_game_cost(ordinals, threads)
+        out["per_game_cost"] = per_game_cost(ordinals, threads, games_per_rank)
     runner.close()   # frees the games' trees before the CPU baseline
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:

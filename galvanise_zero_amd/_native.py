@@ -313,7 +313,9 @@ class GzOrdinalStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_long * GZ_ORDINALS) for n in ("games", "evals", "tree_playouts", "moves", "spin_epochs")] + \
                [("engine_s", ctypes.c_double * GZ_ORDINALS), ("cost_hist", ctypes.c_long * GZ_COST_HIST),
                 ("inflight_games", ctypes.c_long), ("inflight_engine_s", ctypes.c_double),
-                ("inflight_evals", ctypes.c_long)]
+                ("inflight_evals", ctypes.c_long), ("inflight_games_ord", ctypes.c_long * GZ_ORDINALS),
+                ("inflight_engine_s_ord", ctypes.c_double * GZ_ORDINALS),
+                ("inflight_evals_ord", ctypes.c_long * GZ_ORDINALS)]
 
     def as_dict(self):
         out = {}

@@ -521,12 +521,17 @@ extern "C" int gz_pool_add_ordinal_stats(gz_pool* p, gz_ordinal_stats* out) {
         out->engine_s[k] += (double)o.cycles[k] / hz;
     }
     for (int k = 0; k < GZ_COST_HIST; ++k) out->cost_hist[k] += o.cost_hist[k];
-    long g = 0, e = 0;
-    double s = 0;
-    p->impl->inflight(&g, &s, &e);
-    out->inflight_games += g;
-    out->inflight_engine_s += s;
-    out->inflight_evals += e;
+    long g[GZ_ORDINALS], e[GZ_ORDINALS];
+    double s[GZ_ORDINALS];
+    p->impl->inflight(g, s, e);
+    for (int k = 0; k < GZ_ORDINALS; ++k) {
+        out->inflight_games += g[k];
+        out->inflight_engine_s += s[k];
+        out->inflight_evals += e[k];
+        out->inflight_games_ord[k] += g[k];
+        out->inflight_engine_s_ord[k] += s[k];
+        out->inflight_evals_ord[k] += e[k];
+    }
     return 0;
 }
 extern "C" int gz_engine_set_verify_fastpath(int on) {

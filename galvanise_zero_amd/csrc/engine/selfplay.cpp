@@ -347,19 +347,19 @@ void SelfPlayManager::startSelfPlayers(const SelfPlayConfig* config) {
 }
 
 void SelfPlayManager::inflight(long* games, double* engine_s, long* evals) const {
-    long g = 0, e = 0;
-    uint64_t c = 0;
+    constexpr int K = OrdinalStats::kOrdinals;
+    uint64_t c[K] = {};
+    for (int k = 0; k < K; ++k) games[k] = evals[k] = 0;
     for (size_t i = 0; i < self_plays.size(); ++i) {
         const SelfPlay* sp = self_plays[i];
         if (sp->coro == nullptr) continue;
-        g++;
+        const int k = std::min(std::max(sp->matchCount(), 1), K) - 1;
+        games[k]++;
         const uint64_t now = sp->coro->cycles;   // as of the coroutine's last switch
-        if (now > sp->game_c0) c += now - sp->game_c0;
-        e += evaluators[i]->totalEvaluations() - sp->game_e0;
+        if (now > sp->game_c0) c[k] += now - sp->game_c0;
+        evals[k] += evaluators[i]->totalEvaluations() - sp->game_e0;
     }
-    *games = g;
-    *engine_s = (double)c / tsc_hz();
-    *evals = e;
+    for (int k = 0; k < K; ++k) engine_s[k] = (double)c[k] / tsc_hz();
 }
 
 void SelfPlayManager::poll() {

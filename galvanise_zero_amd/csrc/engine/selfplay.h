@@ -69,7 +69,7 @@ public:
              const uint64_t* initial_state, int role_count, std::string identifier, uint64_t seed);
     void playOnce();
     void playGamesForever();
-    int matchCount() const { return match_count; }
+    int matchCount() const { return match_count; }   // games started (the current one included)
 
 private:
     bool resign(const PuctNode* node);
@@ -169,7 +169,8 @@ public:
     void startSelfPlayers(const SelfPlayConfig* config);
     void poll();
 
-    // games in progress: count, engine seconds and evaluations they have used so far
+    // games in progress by ordinal (OrdinalStats::kOrdinals buckets): count, engine seconds and
+    // evaluations they have used so far
     void inflight(long* games, double* engine_s, long* evals) const;
 
     std::vector<Sample*>& getSamples() { return samples; }

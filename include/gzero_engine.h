@@ -115,6 +115,9 @@ typedef struct gz_ordinal_stats {
     long inflight_games;              /* games in progress at the snapshot */
     double inflight_engine_s;         /* engine seconds they have used so far */
     long inflight_evals;              /* evaluations they have used so far */
+    long inflight_games_ord[GZ_ORDINALS];      /* the same by the in-progress game's ordinal */
+    double inflight_engine_s_ord[GZ_ORDINALS];
+    long inflight_evals_ord[GZ_ORDINALS];
 } gz_ordinal_stats;
 
 const char* gz_engine_last_error(void);

@@ -72,6 +72,42 @@ def patch(name, text):  # noqa: C901
             "                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[0][t][1], acc[ct][t], 0, 0, 0);\n")
         rep("                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[j & 1][t][0], acc[ct][t], 0, 0, 0);\n",
             "                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[0][t][0], acc[ct][t], 0, 0, 0);\n")
+    elif name == "asmchain":
+        # the looped conv's three split products of one (co tile, position tile) as ONE inline-asm
+        # chain with dst == srcC (the accumulate-forwarding case: no interlock), instead of builtins
+        # the register allocator renames (dst != srcC, copies at the loop top); s_nop 1 first (a VALU
+        # write of an operand right before), s_nop 15 after each conv (VALU reads of the last D)
+        rep("""                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][0], acc[ct][t], 0, 0, 0);
+                    if constexpr (P2 == 2) {
+                        const bf16x8 w_lo = ring.r[ST % R][k][ct * WP + 1];
+                        acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][1], acc[ct][t], 0, 0, 0);
+                        acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[t][0], acc[ct][t], 0, 0, 0);
+                    }
+""", """                    if constexpr (P2 == 2) {
+                        const bf16x8 w_lo = ring.r[ST % R][k][ct * WP + 1];
+                        asm volatile("s_nop 1\\n\\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\\n\\t"
+                                     "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\\n\\t"
+                                     "v_mfma_f32_16x16x32_bf16 %0, %4, %2, %0"
+                                     : "+a"(acc[ct][t]) : "v"(w_hi), "v"(b[t][0]), "v"(b[t][1]), "v"(w_lo));
+                    } else {
+                        acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][0], acc[ct][t], 0, 0, 0);
+                    }
+""")
+        rep("""                __builtin_amdgcn_sched_group_barrier(0x008, CT * (P2 == 2 ? 3 : 1), 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, P2, 0);                       // DS read
+            }
+        __builtin_amdgcn_sched_barrier(0);""", """            }
+        __builtin_amdgcn_sched_barrier(0);""")
+        rep("""        conv_iter<F, PTN, NB, P, WG>(X, ring, acc, b, wres, woff, gs0 + it * G::U, gmax, lane, bd, it * G::TPI,
+                                 it == G::NIT - 1, std::make_integer_sequence<int, G::U>{});
+""", """        conv_iter<F, PTN, NB, P, WG>(X, ring, acc, b, wres, woff, gs0 + it * G::U, gmax, lane, bd, it * G::TPI,
+                                 it == G::NIT - 1, std::make_integer_sequence<int, G::U>{});
+    asm volatile("s_nop 15" ::: "memory");
+""")
+    elif name == "asmchain_nonop":
+        # asmchain without the leading s_nop 1 (the operands come from loads, not VALU writes)
+        text = patch("asmchain", text)
+        rep('asm volatile("s_nop 1\\n\\tv_mfma_f32_16x16x32_bf16', 'asm volatile("v_mfma_f32_16x16x32_bf16')
     elif "+" in name:
         for part in name.split("+"):
             text = patch(part, text)

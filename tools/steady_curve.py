@@ -75,6 +75,14 @@ def main():
                "samples_per_s": d["samples"] / dt, "dupes_per_s": d["dupes"] / dt, "rolls": rolls,
                "rss_gb": rss_gb(),
                "evals_per_game_cum": st["completed_game_evals"] / max(1, st["games_completed"])}
+        # per-ordinal game costs (gz_ordinal_stats): completed games and the games in progress, by
+        # the game's ordinal within its slot -- the first-game cohort (ordinal 1, one per slot)
+        # completes over the run, and its costs bound the stationary per-game cost
+        o = r.ordinal_stats()
+        row["ordinals"] = {k: o[k] for k in ("games", "evals", "tree_playouts", "engine_s", "inflight_games_ord",
+                                             "inflight_engine_s_ord", "inflight_evals_ord")}
+        row["engine_s_in_games"] = sum(o["engine_s"]) + o["inflight_engine_s"]
+        row["thread_s"] = threads * (now - t0)
         rows_log.append(row)
         print(json.dumps(row), flush=True)
         prev, tp = st, now
