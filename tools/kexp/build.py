@@ -10,7 +10,9 @@ libgz_engine.so.  Timing on the GPU box: GZ_LIB_DIR=tools/kexp/lib_<name> python
   nobarrier    no workgroup barrier after the residual epilogues (results wrong; barrier cost)
   noaddr       every tap reads the centre tap's B addresses (no per-tap address arithmetic)
   noreads      no B-fragment LDS reads after each conv's first k-step
+  siunroll     the single-image kernels' fully unrolled conv (round 3) instead of the looped one
   a+b          both patches
+  full_<name>  patch <name>, build every trunk instantiation (the deep configs' F = 256 kernels)
 Usage: python tools/kexp/build.py base nostore ...
 """
 import os
@@ -58,6 +60,9 @@ def patch(name, text):  # noqa: C901
             "            }\n        }\n        __syncthreads();\n    }\n",
             "                store_act<F, PTN, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);\n"
             "            }\n        }\n    }\n")
+    elif name == "siunroll":
+        rep("    static constexpr bool LOOPSI = SI && NST % US == 0 && NST / US >= 2;\n",
+            "    static constexpr bool LOOPSI = false;\n")
     elif name == "unroll":
         rep("    static constexpr bool LOOP = !SI && NST % U == 0 && NIT >= 2;\n", "    static constexpr bool LOOP = false;\n")
     elif name == "noaddr":
@@ -117,6 +122,7 @@ def patch(name, text):  # noqa: C901
 
 
 def build(name):
+    full = name.startswith("full_")
     work = "/tmp/kexp_" + name
     shutil.rmtree(work, ignore_errors=True)
     shutil.copytree(SRC, os.path.join(work, "nn"))
@@ -129,9 +135,10 @@ def build(name):
         p = os.path.join(nn, f)
         t = open(p).read().replace("../../../include/", "../include/")
         if f == "forward_kernel.h":
-            t = patch(name, t)
+            t = patch(name[5:] if full else name, t)
         open(p, "w").write(t)
-    open(os.path.join(nn, "trunk_exp.hip"), "w").write(STUB)
+    if not full:
+        open(os.path.join(nn, "trunk_exp.hip"), "w").write(STUB)
     out = os.path.join(ROOT, "tools", "kexp", "lib_" + name)
     os.makedirs(out, exist_ok=True)
     eng = os.path.join(out, "libgz_engine.so")
@@ -140,7 +147,8 @@ def build(name):
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-parameter"]
     objs = []
     procs = []
-    for tu in ("gz_nn.hip", "runner.hip", "trunk_exp.hip"):
+    tus = ["gz_nn.hip", "runner.hip"] + (sorted(f for f in os.listdir(nn) if f.startswith("trunk_f")) if full else ["trunk_exp.hip"])
+    for tu in tus:
         o = os.path.join(work, tu + ".o")
         objs.append(o)
         procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc"] + flags + ["-c", "-o", o, os.path.join(nn, tu)]))
