@@ -65,7 +65,7 @@ PMC_PER_LAUNCH = {"gznn::trunk_kernel<128, 4, 2, 1, 3>": {
               "1024-row launches, tools/gpu_pmc_r04.sh): busy cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)"}}
 
 
-def per_game_cost(o, threads, slots):
+def per_game_cost(o, threads, slots, run_s):
     """Per-game cost by the game's ordinal within its slot (gz_ordinal_stats of rank 0's runner, the
     whole run): is a slot's k-th game dearer than its first?  Plus the first-game cohort (ordinal 1:
     one game per slot, every game an independent draw from the initial position with its own RNG
@@ -94,7 +94,19 @@ def per_game_cost(o, threads, slots):
               "evals_completed": o["evals"][0], "evals_in_progress": o["inflight_evals_ord"][0],
               "mean_engine_ms_per_game_lower_bound": 1e3 * c_s / slots if slots else None,
               "evals_per_engine_s_so_far": c_e / c_s if c_s > 0 else None}
+    # stationary rate (renewal-reward over games): threads x f x E[evals / game] / E[engine-s / game],
+    # f = the share of the engine threads' time spent inside game coroutines over the run.  From the
+    # completed games (VERDICT r03 item 3's estimate: biased towards cheap games, an upper bound) and
+    # from the first-game cohort so far (completed + in-progress: every slot's first game)
+    in_game_s = es + o["inflight_engine_s"]
+    f = in_game_s / (threads * run_s) if run_s > 0 and threads else None
+    stationary = {"in_game_thread_share": f, "run_s": run_s,
+                  "from_completed_games_leaf_evals_per_s": threads * f * ev / es if f and es > 0 else None,
+                  "from_first_game_cohort_leaf_evals_per_s": threads * f * c_e / c_s if f and c_s > 0 else None,
+                  "note": "completed games are the cheap part of a heavy-tailed per-game cost (DESIGN.md section 6): "
+                          "the first figure overstates the stationary rate"}
     return {"by_ordinal": rows, "engine_ms_histogram": hist, "first_game_cohort": cohort,
+            "stationary_estimate": stationary,
             "completed_games_evals_per_engine_s": ev / es if es > 0 else None,
             "in_progress": {"games": o["inflight_games"], "engine_s": o["inflight_engine_s"],
                             "evals": o["inflight_evals"],
@@ -399,6 +411,7 @@ def main():
     s1 = runner.stats()
     t1 = time.perf_counter()
     ordinals = runner.ordinal_stats()
+    run_s = time.perf_counter() - t_start
     barrier()
     runner.stop()
     elapsed = t1 - t0
@@ -560,7 +573,7 @@ def main():
                 gbps = out["roofline"]["traffic"] / (per_variant[dom]["avg_kernel_ms"] / 1e3) / 1e9
                 out["roofline"].update({"mfma_busy_frac": busy, "hbm_GBps": gbps, "hbm_peak_GBps": PEAK_HBM_GBPS,
                                         "hbm_frac": gbps / PEAK_HBM_GBPS, "pmc_source": pmc["source"]})
-        out["per_game_cost"] = per_game_cost(ordinals, threads, games_per_rank)
+        out["per_game_cost"] = per_game_cost(ordinals, threads, games_per_rank, run_s)
     runner.close()   # frees the games' trees before the CPU baseline
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:

@@ -119,3 +119,26 @@ def test_verify_switch_on_live_pool():
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert r["before"] == 0 and r["during"] > 1000 and r["after"] == 0, r
+
+
+def test_bench_per_game_cost_stationary_estimate():
+    """bench.py's per-game cost summary: by-ordinal rows, first-game cohort and the stationary
+    estimates (threads x in-game share x evals per engine-second) from a synthetic counter set."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    K = 8
+    o = {"games": [10, 4] + [0] * (K - 2), "evals": [1000.0, 400.0] + [0.0] * (K - 2),
+         "tree_playouts": [5000.0, 2000.0] + [0.0] * (K - 2), "moves": [100.0, 40.0] + [0.0] * (K - 2),
+         "spin_epochs": [3.0, 1.0] + [0.0] * (K - 2), "engine_s": [2.0, 1.0] + [0.0] * (K - 2),
+         "cost_hist": [0] * 32, "inflight_games": 6, "inflight_engine_s": 5.0, "inflight_evals": 300.0,
+         "inflight_games_ord": [2, 4] + [0] * (K - 2), "inflight_engine_s_ord": [3.0, 2.0] + [0.0] * (K - 2),
+         "inflight_evals_ord": [100.0, 200.0] + [0.0] * (K - 2)}
+    r = bench.per_game_cost(o, threads=2, slots=12, run_s=5.0)
+    assert [row["ordinal"] for row in r["by_ordinal"]] == [1, 2]
+    assert r["by_ordinal"][0]["evals_per_game"] == 100.0
+    st = r["stationary_estimate"]
+    f = (3.0 + 5.0) / (2 * 5.0)
+    assert st["in_game_thread_share"] == pytest.approx(f)
+    assert st["from_completed_games_leaf_evals_per_s"] == pytest.approx(2 * f * 1400.0 / 3.0)
+    assert st["from_first_game_cohort_leaf_evals_per_s"] == pytest.approx(2 * f * 1100.0 / 5.0)
+    assert r["first_game_cohort"]["mean_engine_ms_per_game_lower_bound"] == pytest.approx(1e3 * 5.0 / 12)
