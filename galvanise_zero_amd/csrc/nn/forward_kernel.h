@@ -196,11 +196,10 @@ struct Geo {
     static constexpr int NST = 9 * KC / KS;          // ring stages per conv
     // ring depth; the two-board split kernels take exactly one tap's stages (R = KC / KS) so the
     // looped conv's body is one tap (a deeper ring made the body three taps and spilled)
-    static constexpr int R = (P2 == 2 && (NB == 2 || WG == 2) && (KC / KS) >= 3 && NST % (KC / KS) == 0 &&
-                              (KC / KS) * KS * NFR * 4 <= 96)
-                                 ? KC / KS
-                                 : ring_depth(NST, KS, NFR, CT >= 4 ? 64 : 96);
-    static constexpr int LPS = KS * NFR;             // weight loads per stage per lane
+    static constexpr int R0 = (P2 == 2 && (NB == 2 || WG == 2) && (KC / KS) >= 3 && NST % (KC / KS) == 0 &&
+                               (KC / KS) * KS * NFR * 4 <= 96)
+                                  ? KC / KS
+                                  : ring_depth(NST, KS, NFR, CT >= 4 ? 64 : 96);
     // Single-image mode: when two ping-pong images (+ bias table) do not fit the 160 KB of LDS
     // (F = 256 on 10x10 / 13x13 boards), or the registers are nearly full anyway (large boards:
     // the single-image epilogue keeps fewer values live), one image is overwritten in place: every conv's MFMAs
@@ -208,8 +207,16 @@ struct Geo {
     // scratch then alias the image.
     // live VGPRs of the trunk loop: weight ring + double-buffered B fragments + accumulators +
     // residual stream
-    static constexpr int LIVE_VGPRS = R * KS * NFR * 4 + 2 * TT * P2 * 4 + 2 * CT * TT * 4;
+    static constexpr int LIVE_VGPRS = R0 * KS * NFR * 4 + 2 * TT * P2 * 4 + 2 * CT * TT * 4;
     static constexpr bool SI = 2 * NB * ACT_BYTES + 16 * 1024 > 160 * 1024 || (NB == 1 && LIVE_VGPRS > 330);
+    // ring depth: single-image kernels run the looped conv (single-buffered B fragments), which
+    // leaves room for a deeper ring (up to 128 VGPRs: F = 256 split, 4 stages = 3 k-steps ahead of
+    // the MFMAs; its weights stream from the MALL, not the L2)
+    static constexpr int RS = ring_depth(NST, KS, NFR, 64);
+    static constexpr int US = lcm_c(RS, KC / KS) * ((lcm_c(RS, KC / KS) * KS) % 2 ? 2 : 1);
+    static constexpr bool LOOPSI = SI && NST % US == 0 && NST / US >= 2;
+    static constexpr int R = LOOPSI ? RS : R0;
+    static constexpr int LPS = KS * NFR;             // weight loads per stage per lane
     // Global residual: when the fp32 residual stream (+ the accumulators) would need more than 256
     // VGPRs (F = 256 on 13x13: 2 x 176), it lives in a per-workgroup device scratch instead of
     // registers, lane-contiguous (one coalesced 1 KB store / load per wave and tile).
@@ -240,6 +247,7 @@ struct Geo {
     static constexpr int NIT = NST / U;
     static constexpr int TPI = U * KS / KC;                              // taps per iteration
     static constexpr bool LOOP = !SI && NST % U == 0 && NIT >= 2;
+    static_assert(!LOOPSI || (NST % U == 0 && NIT >= 2), "single-image looped conv");
 };
 
 // chunk rotation of LDS row q (q may be a virtual, off-board position)
@@ -354,24 +362,25 @@ template <int WP, int ROWB, int FR>
 struct FragOff {
     static constexpr int value = (FR / WP) * 16 * ROWB + (FR % WP) * 64;
 };
-template <int F, int PTN, int NB, int P, int WG, int SLOT, bool HI_ONLY, int FR>
+template <int F, int PTN, int NB, int P, int WG, int SLOT, int PARTS, int FR>
 __device__ __forceinline__ void ring_issue_f(Ring<F, PTN, NB, P, WG>& ring, int k, uint32_t woff, const char* sb) {
     using G = Geo<F, PTN, NB, P, WG>;
-    if constexpr (!HI_ONLY || FR % G::WP == 0) {
+    if constexpr ((PARTS >> (FR % G::WP)) & 1) {
         if constexpr (G::TRACKED)
             ring.r[SLOT][k][FR] = *(const bf16x8*)(sb + woff + FragOff<G::WP, G::ROWB, FR>::value);
         else
             ring.r[SLOT][k][FR] = gload_issue<FragOff<G::WP, G::ROWB, FR>::value>(woff, sb);
     }
 }
-template <int F, int PTN, int NB, int P, int WG, int SLOT, bool HI_ONLY, int... FRS>
+template <int F, int PTN, int NB, int P, int WG, int SLOT, int PARTS, int... FRS>
 __device__ __forceinline__ void ring_issue_k(Ring<F, PTN, NB, P, WG>& ring, int k, uint32_t woff, const char* sb,
                                              std::integer_sequence<int, FRS...>) {
-    (ring_issue_f<F, PTN, NB, P, WG, SLOT, HI_ONLY, FRS>(ring, k, woff, sb), ...);
+    (ring_issue_f<F, PTN, NB, P, WG, SLOT, PARTS, FRS>(ring, k, woff, sb), ...);
 }
-// HI_ONLY (P = 2, a stage of a conv's second pass, which multiplies by the hi parts only): the lo
-// fragments are not loaded (their slot registers are not read in that pass; TRACKED kernels only)
-template <int F, int PTN, int NB, int P, int WG, int SLOT, bool HI_ONLY = false>
+// PARTS: bit 0 the hi fragments, bit 1 the lo fragments.  P = 2: a stage of a conv's second pass
+// multiplies by the hi parts only, so its lo fragments are not loaded (their slot registers are not
+// read in that pass; TRACKED kernels only)
+template <int F, int PTN, int NB, int P, int WG, int SLOT, int PARTS = 3>
 __device__ __forceinline__ void ring_issue(Ring<F, PTN, NB, P, WG>& ring, const __bf16* wres, uint32_t woff, int gs, int gmax) {
     using G = Geo<F, PTN, NB, P, WG>;
     int s = gs < gmax ? gs : gmax;
@@ -380,7 +389,7 @@ __device__ __forceinline__ void ring_issue(Ring<F, PTN, NB, P, WG>& ring, const 
     if constexpr (P == 2) s = (s / (2 * G::NST)) * G::NST + s % G::NST;
 #pragma unroll
     for (int k = 0; k < G::KS; ++k)
-        ring_issue_k<F, PTN, NB, P, WG, SLOT, HI_ONLY>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * G::ROWB,
+        ring_issue_k<F, PTN, NB, P, WG, SLOT, PARTS>(ring, k, woff, (const char*)wres + (size_t)(s * G::KS + k) * F * G::ROWB,
                                                     std::make_integer_sequence<int, G::NFR>{});
 }
 
@@ -436,7 +445,7 @@ __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, P
     // next one; the second pass's stages need the hi parts only
     constexpr bool next_in_pass = ST + R - 1 < G::NST;
     constexpr bool hi_only = P == 2 && G::TRACKED && (next_in_pass ? PASS == 1 : PASS == 0);
-    ring_issue<F, PTN, NB, P, WG, (ST + R - 1) % R, hi_only>(ring, wres, woff, gs0 + ST + R - 1, gmax);
+    ring_issue<F, PTN, NB, P, WG, (ST + R - 1) % R, hi_only ? 1 : 3>(ring, wres, woff, gs0 + ST + R - 1, gmax);
     if constexpr (!G::TRACKED) {
         ring_wait<(R - 1) * G::LPS>();
 #pragma unroll
@@ -544,7 +553,11 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN,
 // after tile t's last MFMA of this k-step (the other tiles' MFMAs, ~670 cycles, cover the LDS
 // latency), which saves the 64 VGPRs of a second buffer; the register allocator otherwise shuffled
 // loop-carried values between VGPRs and AGPRs every iteration.
-template <int F, int PTN, int NB, int P, int WG, int ST>
+// P = 2 (two-pass split, PASS 0 / 1; single-image kernels): pass 0 multiplies the hi image by the hi
+// and lo weights, pass 1 the lo image by the hi weights only, so pass 1 loads no lo fragments -- except
+// where a stage of the last iteration looks ahead into the next conv's pass 0 (and pass 0's look-ahead
+// into pass 1 skips them): a uniform branch on last_it around those loads.
+template <int F, int PTN, int NB, int P, int WG, int PASS, int ST>
 __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                              f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                              bf16x8 (&b)[Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
@@ -552,9 +565,20 @@ __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F,
                                              const Board& bd, int tap0, bool last_it) {
     using G = Geo<F, PTN, NB, P, WG>;
     constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, KC = G::KC, P2 = G::P2, WP = G::WP;
-    static_assert(P != 2, "two-pass split precision runs the single-image conv");
+    static_assert(P != 2 || G::TRACKED, "two-pass split: compiler-tracked weight loads");
     static_assert(G::U % R == 0, "ring slots must be static within an iteration");
-    ring_issue<F, PTN, NB, P, WG, (ST + R - 1) % R>(ring, wres, woff, gs_it + ST + R - 1, gmax);
+    if constexpr (P == 2) {
+        constexpr int SLOT = (ST + R - 1) % R;
+        const int gs = gs_it + ST + R - 1;
+        ring_issue<F, PTN, NB, P, WG, SLOT, 1>(ring, wres, woff, gs, gmax);
+        if constexpr (ST + R - 1 < G::U) {    // a stage of this iteration's pass
+            if constexpr (PASS == 0) ring_issue<F, PTN, NB, P, WG, SLOT, 2>(ring, wres, woff, gs, gmax);
+        } else if ((PASS == 0) != last_it) {  // the next iteration's, or the next pass's (last_it)
+            ring_issue<F, PTN, NB, P, WG, SLOT, 2>(ring, wres, woff, gs, gmax);
+        }
+    } else {
+        ring_issue<F, PTN, NB, P, WG, (ST + R - 1) % R>(ring, wres, woff, gs_it + ST + R - 1, gmax);
+    }
     if constexpr (!G::TRACKED) {
         ring_wait<(R - 1) * G::LPS>();
 #pragma unroll
@@ -583,6 +607,9 @@ __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F,
                         const bf16x8 w_lo = ring.r[ST % R][k][ct * WP + 1];
                         acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][1], acc[ct][t], 0, 0, 0);
                         acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[t][0], acc[ct][t], 0, 0, 0);
+                    } else if constexpr (P == 2 && PASS == 0) {   // + lo*hi (pass 1: hi*lo only)
+                        const bf16x8 w_lo = ring.r[ST % R][k][ct * WP + 1];
+                        acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[t][0], acc[ct][t], 0, 0, 0);
                     }
                 }
                 {   // tile t of the next k-step (unconditional: past the conv's last k-step the tap
@@ -591,33 +618,36 @@ __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F,
 #pragma unroll
                     for (int h = 0; h < P2; ++h) b[t][h] = *(const bf16x8*)(a + h * G::HALF);
                 }
-                __builtin_amdgcn_sched_group_barrier(0x008, CT * (P2 == 2 ? 3 : 1), 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x008, CT * (P2 == 2 ? 3 : P == 2 && PASS == 0 ? 2 : 1), 0);   // MFMA
                 __builtin_amdgcn_sched_group_barrier(0x100, P2, 0);                       // DS read
             }
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-template <int F, int PTN, int NB, int P, int WG, int... ST>
+template <int F, int PTN, int NB, int P, int WG, int PASS, int... ST>
 __device__ __forceinline__ void conv_iter(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                           f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                           bf16x8 (&b)[Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
                                           const __bf16* wres, uint32_t woff, int gs_it, int gmax, int& lane,
                                           const Board& bd, int tap0, bool last_it, std::integer_sequence<int, ST...>) {
-    (conv_stage_l<F, PTN, NB, P, WG, ST>(X, ring, acc, b, wres, woff, gs_it, gmax, lane, bd, tap0, last_it), ...);
+    (conv_stage_l<F, PTN, NB, P, WG, PASS, ST>(X, ring, acc, b, wres, woff, gs_it, gmax, lane, bd, tap0, last_it), ...);
 }
 
-template <int F, int PTN, int NB, int P, int WG = 1>
+// PASS (P = 2): 0 starts the accumulators, 1 adds to them
+template <int F, int PTN, int NB, int P, int WG = 1, int PASS = 0>
 __device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                                f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
                                                const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane,
                                                const Board& bd) {
     using G = Geo<F, PTN, NB, P, WG>;
     constexpr int PT = G::PT, TT = G::TT;
+    if constexpr (PASS == 0) {
 #pragma unroll
-    for (int ct = 0; ct < G::CT; ++ct)
+        for (int ct = 0; ct < G::CT; ++ct)
 #pragma unroll
-        for (int t = 0; t < TT; ++t) acc[ct][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int t = 0; t < TT; ++t) acc[ct][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     bf16x8 b[TT][G::P2];
     launder(lane);
 #pragma unroll
@@ -630,8 +660,8 @@ __device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<
     }
 #pragma clang loop unroll(disable)
     for (int it = 0; it < G::NIT; ++it)
-        conv_iter<F, PTN, NB, P, WG>(X, ring, acc, b, wres, woff, gs0 + it * G::U, gmax, lane, bd, it * G::TPI,
-                                 it == G::NIT - 1, std::make_integer_sequence<int, G::U>{});
+        conv_iter<F, PTN, NB, P, WG, PASS>(X, ring, acc, b, wres, woff, gs0 + it * G::U, gmax, lane, bd, it * G::TPI,
+                                       it == G::NIT - 1, std::make_integer_sequence<int, G::U>{});
 }
 
 // Per-board channel sums over the board's positions of the wave's accumulator tiles: lane group g
@@ -1013,11 +1043,15 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
             const bool second = cv & 1;
             const float* bt = btab + cv * F;
             if constexpr (P == 2) {
-                conv3x3<F, PTN, NB, P, WG, 0>(X0, ring, acc, kp.wres, woff, (2 * cv) * G::NST, gmax, lane, bd);
+                if constexpr (G::LOOPSI) conv3x3_looped<F, PTN, NB, P, WG, 0>(X0, ring, acc, kp.wres, woff, (2 * cv) * G::NST, gmax, lane, bd);
+                else conv3x3<F, PTN, NB, P, WG, 0>(X0, ring, acc, kp.wres, woff, (2 * cv) * G::NST, gmax, lane, bd);
                 __syncthreads();    // every wave has finished reading the hi image
                 lo_copy<F, PTN, true>(X0, xlo, NPOS, tid);   // the lo image
                 __syncthreads();
-                conv3x3<F, PTN, NB, P, WG, 1>(X0, ring, acc, kp.wres, woff, (2 * cv + 1) * G::NST, gmax, lane, bd);
+                if constexpr (G::LOOPSI) conv3x3_looped<F, PTN, NB, P, WG, 1>(X0, ring, acc, kp.wres, woff, (2 * cv + 1) * G::NST, gmax, lane, bd);
+                else conv3x3<F, PTN, NB, P, WG, 1>(X0, ring, acc, kp.wres, woff, (2 * cv + 1) * G::NST, gmax, lane, bd);
+            } else if constexpr (G::LOOPSI) {
+                conv3x3_looped<F, PTN, NB, P, WG>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane, bd);
             } else {
                 conv3x3<F, PTN, NB, P, WG>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane, bd);
             }
