@@ -135,6 +135,11 @@ struct Board {
     __device__ __forceinline__ int row(int p) const { return (p * wmagic) >> 16; }
 };
 
+// Single-image kernels with the looped conv (deeper ring, single-buffered B fragments): measured
+// slower than their fully unrolled conv on MI355X (cfg4 12.9 -> 14.6 ms, cfg5 equal at 1,024 rows,
+// bit-identical; profiles/r04e_kexp.txt), so off; kept for experiments (tools/kexp siloop)
+constexpr bool kLoopSI = false;
+
 // ring depth: largest R dividing the stages per conv with R slots of KS*CT fragments <= cap VGPRs
 __host__ __device__ constexpr int ring_depth(int nst, int ks, int ct, int cap) {
     const int cand[5] = {9, 6, 4, 3, 2};
@@ -214,7 +219,7 @@ struct Geo {
     // the MFMAs; its weights stream from the MALL, not the L2)
     static constexpr int RS = ring_depth(NST, KS, NFR, 64);
     static constexpr int US = lcm_c(RS, KC / KS) * ((lcm_c(RS, KC / KS) * KS) % 2 ? 2 : 1);
-    static constexpr bool LOOPSI = SI && NST % US == 0 && NST / US >= 2;
+    static constexpr bool LOOPSI = kLoopSI && SI && NST % US == 0 && NST / US >= 2;
     static constexpr int R = LOOPSI ? RS : R0;
     static constexpr int LPS = KS * NFR;             // weight loads per stage per lane
     // Global residual: when the fp32 residual stream (+ the accumulators) would need more than 256
@@ -557,6 +562,45 @@ __device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN,
 // and lo weights, pass 1 the lo image by the hi weights only, so pass 1 loads no lo fragments -- except
 // where a stage of the last iteration looks ahead into the next conv's pass 0 (and pass 0's look-ahead
 // into pass 1 skips them): a uniform branch on last_it around those loads.
+// The split product of one (co tile, position tile) in the looped conv -- hi*hi + hi*lo + lo*hi --
+// as ONE inline-asm accumulate chain with dst == srcC.  With the builtins the register allocator
+// renamed accumulators across the loop (dst != srcC, then VGPR / AGPR copies at the loop top); the
+// chain keeps every accumulator in its AGPRs (-4 % launch time at 1,024 rows, bit-identical,
+// profiles/r04e_kexp.txt).  Hazards (nothing inside an asm string is padded by the compiler): an
+// MFMA taking the previous MFMA's D whole as C needs no wait states; the A/B operands come from
+// LDS / global loads (no VALU write before the chain; tests/test_kernel_asm_audit.py checks the
+// compiled kernels for copies into them or accesses to the accumulators inside the loop); the
+// accumulators' zeroing and the epilogue's reads are fenced by split_chain_enter / _leave.
+__device__ __forceinline__ void mfma_split3(f32x4& acc, const bf16x8& wh, const bf16x8& bh, const bf16x8& bl,
+                                            const bf16x8& wl) {
+    asm volatile(
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %4, %2, %0"
+        : "+a"(acc)
+        : "v"(wh), "v"(bh), "v"(bl), "v"(wl));
+}
+// before the first chain: every accumulator is materialised (its zeroing, a VALU write) ahead of a
+// 2-state pad (VALU write -> MFMA operand)
+template <int CT, int TT>
+__device__ __forceinline__ void split_chain_enter(f32x4 (&acc)[CT][TT]) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int t = 0; t < TT; ++t) asm volatile("" : "+a"(acc[ct][t]));
+    asm volatile("s_nop 1" ::: "memory");
+}
+// after the last chain: 24 states (an MFMA's D -> any other reader or writer: 12 for 8 passes, 19 for
+// 16), then every accumulator redefined, so no read of one is scheduled above the pad
+template <int CT, int TT>
+__device__ __forceinline__ void split_chain_leave(f32x4 (&acc)[CT][TT]) {
+    asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int t = 0; t < TT; ++t) asm volatile("" : "+a"(acc[ct][t]));
+}
+
 template <int F, int PTN, int NB, int P, int WG, int PASS, int ST>
 __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                              f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
@@ -602,14 +646,14 @@ __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F,
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct) {
                     const bf16x8 w_hi = ring.r[ST % R][k][ct * WP];
-                    acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][0], acc[ct][t], 0, 0, 0);
                     if constexpr (P2 == 2) {
-                        const bf16x8 w_lo = ring.r[ST % R][k][ct * WP + 1];
-                        acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][1], acc[ct][t], 0, 0, 0);
-                        acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[t][0], acc[ct][t], 0, 0, 0);
-                    } else if constexpr (P == 2 && PASS == 0) {   // + lo*hi (pass 1: hi*lo only)
-                        const bf16x8 w_lo = ring.r[ST % R][k][ct * WP + 1];
-                        acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[t][0], acc[ct][t], 0, 0, 0);
+                        mfma_split3(acc[ct][t], w_hi, b[t][0], b[t][1], ring.r[ST % R][k][ct * WP + 1]);
+                    } else {
+                        acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_hi, b[t][0], acc[ct][t], 0, 0, 0);
+                        if constexpr (P == 2 && PASS == 0) {   // + lo*hi (pass 1: hi*lo only)
+                            const bf16x8 w_lo = ring.r[ST % R][k][ct * WP + 1];
+                            acc[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w_lo, b[t][0], acc[ct][t], 0, 0, 0);
+                        }
                     }
                 }
                 {   // tile t of the next k-step (unconditional: past the conv's last k-step the tap
@@ -618,8 +662,10 @@ __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F,
 #pragma unroll
                     for (int h = 0; h < P2; ++h) b[t][h] = *(const bf16x8*)(a + h * G::HALF);
                 }
-                __builtin_amdgcn_sched_group_barrier(0x008, CT * (P2 == 2 ? 3 : P == 2 && PASS == 0 ? 2 : 1), 0);   // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x100, P2, 0);                       // DS read
+                if constexpr (P2 == 1) {   // (the asm chains are not MFMAs to the scheduler)
+                    __builtin_amdgcn_sched_group_barrier(0x008, CT * (P == 2 && PASS == 0 ? 2 : 1), 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, P2, 0);                                 // DS read
+                }
             }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -658,10 +704,12 @@ __device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<
 #pragma unroll
             for (int h = 0; h < G::P2; ++h) b[bb * PT + pt][h] = *(const bf16x8*)(a + bb * G::ACT_BYTES + h * G::HALF);
     }
+    if constexpr (G::P2 == 2) split_chain_enter(acc);
 #pragma clang loop unroll(disable)
     for (int it = 0; it < G::NIT; ++it)
         conv_iter<F, PTN, NB, P, WG, PASS>(X, ring, acc, b, wres, woff, gs0 + it * G::U, gmax, lane, bd, it * G::TPI,
                                        it == G::NIT - 1, std::make_integer_sequence<int, G::U>{});
+    if constexpr (G::P2 == 2) split_chain_leave(acc);
 }
 
 // Per-board channel sums over the board's positions of the wave's accumulator tiles: lane group g
@@ -997,6 +1045,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         if constexpr (SI) __syncthreads();    // the image overwrites the im2col scratch
         // v2: the image feeding block 0 is the pre-activation act(BN_1(s)) of the stream
         const bool preact = V2 && kp.B > 0;
+        f32x4* rg0 = rg;    // (residual tile addresses formed here, as in the tower's epilogues)
+        if constexpr (RG) launder_ptr(rg0);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const int co = co_base + 16 * ct + 4 * g;
@@ -1016,7 +1066,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                     v[2] = act_fn(v[2], kp.leaky);
                     v[3] = act_fn(v[3], kp.leaky);
                 }
-                if constexpr (RG) rg[(ct * TT + bb * PT + pt) * 64] = v;
+                if constexpr (RG) rg0[(ct * TT + bb * PT + pt) * 64] = v;
                 else resid[ct][bb * PT + pt] = v;
                 acc[ct][bb * PT + pt] = v;    // the heads read acc when there is no residual block
                 store_act<F, PTN, P, !G::SI>(X0 + bb * ACT, 16 * pt + li, co, preact ? pre_act(v, psc, psh, kp.leaky) : v, NPOS);
@@ -1056,9 +1106,15 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                 conv3x3<F, PTN, NB, P, WG>(X0, ring, acc, kp.wres, woff, cv * G::NST, gmax, lane, bd);
             }
             __syncthreads();    // every wave has finished reading the image it is about to overwrite
-            // residual tile addresses are formed here, not hoisted out of the loop (44 x 64-bit)
+            // residual tile addresses are formed here, not hoisted out of the loop (44 x 64-bit);
+            // so are the image's (44 store addresses kept live across the conv spilled)
             f32x4* rgc = rg;
             if constexpr (RG) launder_ptr(rgc);
+            char* Xe = X0;
+            launder_ptr(Xe);
+            int lie = li, ge = g;    // (and their offsets: the lane's row and channel terms)
+            launder(lie);
+            launder(ge);
             if (V2 && second) {   // v2: s += SE(conv2 + bias); image = act(BN_1 of the next block (s))
                 const int blk = cv >> 1;
 #pragma unroll
@@ -1100,7 +1156,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
             }
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
-                const int co = co_base + 16 * ct + 4 * g;
+                const int co = co_base + 16 * ct + 4 * ge;
                 const float4 bias = *(const float4*)(bt + co);
 #pragma unroll
                 for (int t = 0; t < TT; ++t) {
@@ -1121,11 +1177,11 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                         else resid[ct][t] = v;
                     }
                     if (second || P == 2) acc[ct][t] = v;
-                    store_act<F, PTN, P, !G::SI>(X0, 16 * t + li, co, v, NPOS);
+                    store_act<F, PTN, P, !G::SI>(Xe, 16 * t + lie, co, v, NPOS);
                 }
             }
             __syncthreads();
-            if constexpr (P == 2) save_lo_write_hi<F, PTN>(X0, xlo, acc, NPOS, tid, co_base, li, g);
+            if constexpr (P == 2) save_lo_write_hi<F, PTN>(Xe, xlo, acc, NPOS, tid, co_base, lie, ge);
         }
     } else
     for (int blk = 0; blk < kp.B; ++blk) {
