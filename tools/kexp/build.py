@@ -11,6 +11,8 @@ libgz_engine.so.  Timing on the GPU box: GZ_LIB_DIR=tools/kexp/lib_<name> python
   noaddr       every tap reads the centre tap's B addresses (no per-tap address arithmetic)
   noreads      no B-fragment LDS reads after each conv's first k-step
   siunroll     the single-image kernels' fully unrolled conv (round 3) instead of the looped one
+  headsunroll  the dense heads' weight loops unrolled 128 (policy) / 64 (value) instead of 32
+  noheads      the fused trunk kernels skip the dense heads (results wrong; their cost)
   a+b          both patches
   full_<name>  patch <name>, build every trunk instantiation (the deep configs' F = 256 kernels)
 Usage: python tools/kexp/build.py base nostore ...
@@ -60,6 +62,13 @@ def patch(name, text):  # noqa: C901
             "            }\n        }\n        __syncthreads();\n    }\n",
             "                store_act<F, PTN, P>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co, v, NPOS);\n"
             "            }\n        }\n    }\n")
+    elif name == "headsunroll":
+        rep("#pragma unroll 32   // many weight loads in flight: the loop is L2-latency bound\n            for (int k = 0; k < K; ++k) {",
+            "#pragma unroll 128\n            for (int k = 0; k < K; ++k) {")
+        rep("#pragma unroll 32   // many weight loads in flight: the loop is L2-latency bound\n            for (int k = 0; k < VK; ++k) {",
+            "#pragma unroll 64\n            for (int k = 0; k < VK; ++k) {")
+    elif name == "noheads":
+        rep("        dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);", "        if (nb < 0) dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);")
     elif name == "siunroll":
         rep("    static constexpr bool LOOPSI = SI && NST % US == 0 && NST / US >= 2;\n",
             "    static constexpr bool LOOPSI = false;\n")
