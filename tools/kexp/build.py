@@ -13,6 +13,7 @@ libgz_engine.so.  Timing on the GPU box: GZ_LIB_DIR=tools/kexp/lib_<name> python
   siunroll     the single-image kernels' fully unrolled conv (round 3) instead of the looped one
   headsunroll  the dense heads' weight loops unrolled 128 (policy) / 64 (value) instead of 32
   noheads      the fused trunk kernels skip the dense heads (results wrong; their cost)
+  ring6/ring12 the two-board split kernel's weight ring 6 / 12 stages deep instead of one tap (4)
   a+b          both patches
   full_<name>  patch <name>, build every trunk instantiation (the deep configs' F = 256 kernels)
 Usage: python tools/kexp/build.py base nostore ...
@@ -67,6 +68,9 @@ def patch(name, text):  # noqa: C901
             "#pragma unroll 128\n            for (int k = 0; k < K; ++k) {")
         rep("#pragma unroll 32   // many weight loads in flight: the loop is L2-latency bound\n            for (int k = 0; k < VK; ++k) {",
             "#pragma unroll 64\n            for (int k = 0; k < VK; ++k) {")
+    elif name in ("ring6", "ring12"):
+        rep("                                  ? KC / KS\n", "                                  ? %s\n" % ("3 * KC / KS / 2" if name == "ring6" else "3 * KC / KS"))
+        rep("                               (KC / KS) * KS * NFR * 4 <= 96)", "                               (KC / KS) * KS * NFR * 4 <= 96 && NB == 2)")
     elif name == "noheads":
         rep("        dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);", "        if (nb < 0) dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);")
     elif name == "siunroll":
