@@ -962,6 +962,20 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     const int imrow = K0 * 2;
     char* IMlo = IM + align16((NPOS + 1) * imrow);   // split precision: lo parts of the inputs
     const int imswz = ((K0 >> 3) < 16 ? (K0 >> 3) : 16) - 1;
+    // initial-conv weights one k-step ahead of their MFMAs (each step's fragments would otherwise
+    // wait a full L2 round trip); the first step's are the same for every board: issued here, with
+    // the input planes still in flight
+    const int nk0 = K0 >> 5;
+    auto load_w0 = [&](int s, bf16x8 (&x)[CT], bf16x8 (&xl)[CT]) {
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const size_t o = ((size_t)(s * F + co_base + 16 * ct + li)) * 32 + 8 * g;
+            x[ct] = *(const bf16x8*)(kp.w0 + o);
+            if constexpr (IP2 == 2) xl[ct] = *(const bf16x8*)(kp.w0lo + o);
+        }
+    };
+    bf16x8 a0[CT], alo0[CT];
+    load_w0(0, a0, alo0);
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
         const float* in = in_b[bb];
@@ -972,10 +986,12 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         } else {
             for (int i = tid; i < C * NPOS; i += kThreads) sin[i] = in != nullptr ? in[i] : 0.f;
         }
-        __syncthreads();
-        // IM[p][k], k = tap*C + c (a 1x1 initial conv: k = c), zero padded to K0: zero the image,
-        // then one thread per (position, tap) copies its C channels (compile-time divisors only)
-        for (int i = tid; i < IP2 * align16((NPOS + 1) * imrow) / 16; i += kThreads) ((uint4*)IM)[i] = uint4{0u, 0u, 0u, 0u};
+        // IM[p][k], k = tap*C + c (a 1x1 initial conv: k = c), zero padded to K0: zero the image
+        // (beside the planes' staging: disjoint; once per workgroup where the image survives the
+        // board -- the entries the copy below writes depend on the geometry only), then one thread
+        // per (position, tap) copies its C channels (compile-time divisors only)
+        if (SI || bb == 0)
+            for (int i = tid; i < IP2 * align16((NPOS + 1) * imrow) / 16; i += kThreads) ((uint4*)IM)[i] = uint4{0u, 0u, 0u, 0u};
         __syncthreads();
         const int T0 = kp.k0taps;
         for (int i = tid; i < NPOS * T0; i += kThreads) {
@@ -1001,19 +1017,12 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) acc[ct][bb * PT + pt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // initial-conv weights one k-step ahead of their MFMAs (each step's fragments would
-        // otherwise wait a full L2 round trip)
-        const int nk0 = K0 >> 5;
         bf16x8 a[CT], alo[CT];
-        auto load_w0 = [&](int s, bf16x8 (&x)[CT], bf16x8 (&xl)[CT]) {
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                const size_t o = ((size_t)(s * F + co_base + 16 * ct + li)) * 32 + 8 * g;
-                x[ct] = *(const bf16x8*)(kp.w0 + o);
-                if constexpr (IP2 == 2) xl[ct] = *(const bf16x8*)(kp.w0lo + o);
-            }
-        };
-        load_w0(0, a, alo);
+        for (int ct = 0; ct < CT; ++ct) {
+            a[ct] = a0[ct];
+            alo[ct] = alo0[ct];
+        }
         for (int s = 0; s < nk0; ++s) {
             bf16x8 an[CT], alon[CT];
             if (s + 1 < nk0) load_w0(s + 1, an, alon);

@@ -64,8 +64,11 @@ struct Part {
 struct Batch {
     hipEvent_t ev0 = nullptr, evm = nullptr, ev1 = nullptr;
     hipEvent_t evc = nullptr;        // planes copied to d_planes (copy stream)
+    hipEvent_t evk = nullptr;        // output staging: the forward's end (ev1 then follows the copies)
     float* d_planes = nullptr;       // device staging of the batch's planes
     size_t d_cap = 0;                // rows d_planes holds
+    float* d_out = nullptr;          // output staging: the batch's policies and values in HBM
+    size_t d_out_cap = 0;            // rows d_out holds
     std::vector<Part> parts;
     int rows = 0;
 };
@@ -97,6 +100,14 @@ struct gz_runner {
     // GZ_RUNNER_ZERO_COPY=1: the kernel reads the pinned planes directly (the round-1 path).
     hipStream_t copy_stream = nullptr;
     bool zero_copy = false;
+    // Output staging (large policies, e.g. amazons' 3,041 moves): the forward writes its outputs to
+    // HBM and a third stream DMAs them to the pools' pinned buffers, overlapping the next launch,
+    // instead of the heads kernel writing every row over PCIe itself (4 % of cfg5's GPU time).
+    // GZ_RUNNER_OUT_STAGING=0 / 1 overrides the default (on when the policies take >= 1,024 floats
+    // per row).
+    bool out_staging = false;
+    hipStream_t out_stream = nullptr;
+    int out_row_floats = 0;
     Compose compose = kSplit;
     Batch batches_ring[2];
 
@@ -274,7 +285,7 @@ static void launcher_main(gz_runner* r) {
     std::deque<int> inflight;        // indices into batches_ring, oldest first
     int next_slot = 0;
     long launches_issued = 0;
-    std::vector<gz_segment> segs;
+    std::vector<gz_segment> segs, hsegs;
     while (true) {
         // retire finished batches (in order: one stream)
         while (!inflight.empty()) {
@@ -286,7 +297,7 @@ static void launcher_main(gz_runner* r) {
                 return;
             }
             float ms = 0.f;
-            if (hipEventElapsedTime(&ms, b.ev0, b.ev1) == hipSuccess)
+            if (hipEventElapsedTime(&ms, b.ev0, r->out_staging ? b.evk : b.ev1) == hipSuccess)
                 r->kernel_us.fetch_add((long)(ms * 1000.0f), std::memory_order_relaxed);
             if (hipEventElapsedTime(&ms, b.ev0, b.evm) == hipSuccess) {
                 r->trunk_us.fetch_add((long)(ms * 1000.0f), std::memory_order_relaxed);
@@ -519,10 +530,53 @@ static void launcher_main(gz_runner* r) {
                 return;
             }
         }
+        if (r->out_staging) {
+            // the segments' outputs to this slot's HBM staging, [segment][policy 0 .. R-1, value]
+            // blocks of rows x size; the pinned destinations kept for the copies below
+            if (b.d_out_cap < (size_t)b.rows) {
+                if (b.d_out) (void)hipFree(b.d_out);
+                b.d_out = nullptr;
+                const size_t cap = std::max((size_t)b.rows, (size_t)4096);
+                if (hipMalloc((void**)&b.d_out, cap * r->out_row_floats * 4) != hipSuccess) {
+                    set_failed(r, "device output staging allocation failed");
+                    return;
+                }
+                b.d_out_cap = cap;
+            }
+            hsegs = segs;
+            size_t off = 0;
+            for (gz_segment& sg : segs) {
+                for (int j = 0; j < r->num_policies; ++j) {
+                    sg.policies[j] = b.d_out + off;
+                    off += (size_t)sg.rows * r->policy_sizes[j];
+                }
+                sg.values = b.d_out + off;
+                off += (size_t)sg.rows * r->num_values;
+            }
+        }
         if (hipEventRecord(b.ev0, r->stream) != hipSuccess ||
-            gz_net_forward_segments_ev(r->net, r->stream, segs.data(), (int)segs.size(), b.evm) != 0 ||
-            hipEventRecord(b.ev1, r->stream) != hipSuccess) {
+            gz_net_forward_segments_ev(r->net, r->stream, segs.data(), (int)segs.size(), b.evm) != 0) {
             set_failed(r, std::string("launch failed: ") + gz_nn_last_error());
+            return;
+        }
+        if (r->out_staging) {
+            bool ok = hipEventRecord(b.evk, r->stream) == hipSuccess && hipStreamWaitEvent(r->out_stream, b.evk, 0) == hipSuccess;
+            for (size_t k = 0; ok && k < segs.size(); ++k) {
+                const gz_segment& d = segs[k];
+                const gz_segment& h = hsegs[k];
+                if (d.rows == 0) continue;
+                for (int j = 0; ok && j < r->num_policies; ++j)
+                    ok = hipMemcpyAsync(h.policies[j], d.policies[j], (size_t)d.rows * r->policy_sizes[j] * 4,
+                                        hipMemcpyDeviceToHost, r->out_stream) == hipSuccess;
+                ok = ok && hipMemcpyAsync(h.values, d.values, (size_t)d.rows * r->num_values * 4, hipMemcpyDeviceToHost,
+                                          r->out_stream) == hipSuccess;
+            }
+            if (!ok || hipEventRecord(b.ev1, r->out_stream) != hipSuccess) {
+                set_failed(r, "output copy failed");
+                return;
+            }
+        } else if (hipEventRecord(b.ev1, r->stream) != hipSuccess) {
+            set_failed(r, "launch event failed");
             return;
         }
         inflight.push_back(next_slot);
@@ -578,6 +632,12 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
     {
         const char* e = std::getenv("GZ_RUNNER_ZERO_COPY");
         r->zero_copy = e != nullptr && e[0] == '1';
+        int pol_floats = 0;
+        for (int j = 0; j < num_policies; ++j) pol_floats += policy_sizes[j];
+        r->out_row_floats = pol_floats + num_values;
+        r->out_staging = !r->zero_copy && pol_floats >= 1024;
+        if (const char* o = std::getenv("GZ_RUNNER_OUT_STAGING")) r->out_staging = !r->zero_copy && o[0] == '1';
+        if (r->out_staging) ok = ok && hipStreamCreateWithFlags(&r->out_stream, hipStreamNonBlocking) == hipSuccess;
         const char* t = std::getenv("GZ_RUNNER_LEGACY_TRIM");
         if (t != nullptr && t[0] == '1') r->compose = kLegacy;
         if (const char* c = std::getenv("GZ_RUNNER_COMPOSE")) {
@@ -588,7 +648,7 @@ extern "C" gz_runner* gz_runner_create(gz_net* net, const gz_sm* sm, const gz_tr
     for (Batch& b : r->batches_ring)
         ok = ok && hipEventCreate(&b.ev0) == hipSuccess && hipEventCreate(&b.evm) == hipSuccess &&
              hipEventCreateWithFlags(&b.ev1, hipEventBlockingSync) == hipSuccess &&
-             hipEventCreateWithFlags(&b.evc, hipEventDisableTiming) == hipSuccess;
+             hipEventCreateWithFlags(&b.evc, hipEventDisableTiming) == hipSuccess && hipEventCreate(&b.evk) == hipSuccess;
     if (!ok) {
         g_err = "stream / event creation failed";
         gz_runner_destroy(r);
@@ -751,15 +811,19 @@ extern "C" void gz_runner_destroy(gz_runner* r) {
         if (p.h_out) (void)hipHostFree(p.h_out);
     }
     if (r->copy_stream) (void)hipStreamSynchronize(r->copy_stream);
+    if (r->out_stream) (void)hipStreamSynchronize(r->out_stream);
     for (Batch& b : r->batches_ring) {
         if (b.ev0) (void)hipEventDestroy(b.ev0);
         if (b.ev1) (void)hipEventDestroy(b.ev1);
         if (b.evm) (void)hipEventDestroy(b.evm);
         if (b.evc) (void)hipEventDestroy(b.evc);
+        if (b.evk) (void)hipEventDestroy(b.evk);
         if (b.d_planes) (void)hipFree(b.d_planes);
+        if (b.d_out) (void)hipFree(b.d_out);
     }
     if (r->stream) (void)hipStreamDestroy(r->stream);
     if (r->copy_stream) (void)hipStreamDestroy(r->copy_stream);
+    if (r->out_stream) (void)hipStreamDestroy(r->out_stream);
     gz_unique_states_destroy(r->shared_unique);
     delete r;
 }

@@ -14,6 +14,8 @@ libgz_engine.so.  Timing on the GPU box: GZ_LIB_DIR=tools/kexp/lib_<name> python
   headsunroll  the dense heads' weight loops unrolled 128 (policy) / 64 (value) instead of 32
   noheads      the fused trunk kernels skip the dense heads (results wrong; their cost)
   ring6/ring12 the two-board split kernel's weight ring 6 / 12 stages deep instead of one tap (4)
+  lounroll16   the two-pass kernel's lo-image copies 16 uint4 per thread in flight instead of 4
+  nolocopy     the two-pass kernel skips the lo-image copies (results wrong; their cost)
   a+b          both patches
   full_<name>  patch <name>, build every trunk instantiation (the deep configs' F = 256 kernels)
 Usage: python tools/kexp/build.py base nostore ...
@@ -71,6 +73,10 @@ def patch(name, text):  # noqa: C901
     elif name in ("ring6", "ring12"):
         rep("                                  ? KC / KS\n", "                                  ? %s\n" % ("3 * KC / KS / 2" if name == "ring6" else "3 * KC / KS"))
         rep("                               (KC / KS) * KS * NFR * 4 <= 96)", "                               (KC / KS) * KS * NFR * 4 <= 96 && NB == 2)")
+    elif name == "lounroll16":
+        rep("#pragma unroll 4\n    for (int i = tid; i < n16; i += 256) {", "#pragma unroll 16\n    for (int i = tid; i < n16; i += 256) {")
+    elif name == "nolocopy":
+        rep("    for (int i = tid; i < n16; i += 256) {", "    for (int i = tid; i < n16 && npos < 0; i += 256) {")
     elif name == "noheads":
         rep("        dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);", "        if (nb < 0) dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);")
     elif name == "siunroll":
