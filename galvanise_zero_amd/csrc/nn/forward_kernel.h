@@ -86,6 +86,7 @@ struct KParams {
     Segment seg[kMaxSegments];
     unsigned long long* stamps;   // diagnostics only (GZ_KERNEL_STAMPS): [grid][8] s_memtime per phase
     int C, K0, B, R, VH, V, leaky, flatten_nchw, maxP, npos;
+    int lgrow;               // floats per board of the dense heads' LDS outputs (heads_row)
     int H, W, wmagic;        // board rows / columns; wmagic = ceil(65536 / W) (Board::div)
     int value_sigmoid;       // legacy model files: independent sigmoid per value output
     int logits;              // diagnostics (gz_net_set_output_logits): write pre-softmax / pre-sigmoid outputs
@@ -805,10 +806,20 @@ __device__ __forceinline__ void lo_copy(char* X, char* xlo, int npos, int tid) {
     const int n16 = npos * G::ROWS / 16;   // the on-board rows (the zero and scratch rows stay)
     uint4* img = (uint4*)X;
     uint4* glo = (uint4*)xlo;
+    if constexpr (LD) {
+        // LDS-DMA (global_load_lds_dwordx4): each wave-instruction moves 64 consecutive uint4 (1 KB)
+        // from the scratch straight into the image -- no VGPR staging, so every load of the thread is
+        // in flight at once instead of 4 per round trip (the copy was 12 % of cfg4's kernel time)
+        const int lane = tid & 63;
+        for (int i0 = tid - lane; i0 < n16; i0 += 256) {
+            if (i0 + lane < n16)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(glo + i0 + lane),
+                                                 (__attribute__((address_space(3))) void*)(img + i0), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
 #pragma unroll 4
-    for (int i = tid; i < n16; i += 256) {
-        if constexpr (LD) img[i] = glo[i];
-        else glo[i] = img[i];
+        for (int i = tid; i < n16; i += 256) glo[i] = img[i];
     }
 }
 template <int F, int PTN>
@@ -816,7 +827,10 @@ __device__ __forceinline__ void save_lo_write_hi(char* X, char* xlo, const f32x4
                                                  int npos, int tid, int co_base, int li, int g) {
     using G = Geo<F, PTN, 1, 2>;
     lo_copy<F, PTN, false>(X, xlo, npos, tid);
-    __syncthreads();
+    // the image may be overwritten once every wave's LDS reads of it are done; the scratch stores
+    // drain in the background (the next workgroup barrier with a fence, at the end of the next conv's
+    // first pass, orders them before the copy back)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
     for (int ct = 0; ct < G::CT; ++ct)
 #pragma unroll
@@ -1431,10 +1445,10 @@ trunk_kernel_v2(const KParams kp) {
 constexpr int kGemmSoftmaxMax = 3072;   // policy rows the register softmax of gemm_heads takes (48 per lane)
 
 template <int BPW, int NT>
-__device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, float* lg, int board0, int nb) {
+__device__ __forceinline__ void dense_heads_seq(const KParams& kp, const float* fk, float* lg, int board0, int nb) {
     static_assert(BPW >= 1 && BPW <= 4, "one softmax wave per board");
     const int NPOS = kp.npos;
-    const int LMAX = kp.maxP > kp.VH ? kp.maxP : kp.VH;
+    const int LMAX = kp.lgrow;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
     // policy heads: Dense(2HW -> P_r) + softmax
@@ -1486,7 +1500,7 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
             for (int b = 0; b < BPW; ++b) a[b] = 0.f;
 #pragma unroll 32   // many weight loads in flight: the loop is L2-latency bound
             for (int k = 0; k < K; ++k) {
-                const float w = Wd[(size_t)k * P + j];
+                const float w = Wd[(size_t)k * ((P + 3) & ~3) + j];   // rows padded to P4
 #pragma unroll
                 for (int b = 0; b < BPW; ++b) a[b] += fr[k * BPW + b] * w;
             }
@@ -1527,7 +1541,7 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
             for (int b = 0; b < BPW; ++b) a[b] = 0.f;
 #pragma unroll 32   // many weight loads in flight: the loop is L2-latency bound
             for (int k = 0; k < VK; ++k) {
-                const float w = kp.vhw[(size_t)k * VH + j];
+                const float w = kp.vhw[(size_t)k * ((VH + 3) & ~3) + j];
 #pragma unroll
                 for (int b = 0; b < BPW; ++b) a[b] += fv[k * BPW + b] * w;
             }
@@ -1565,12 +1579,187 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
     }
 }
 
+
+// Dense heads in two phases (every config whose policy logits are not longer than the register
+// softmax takes): (A) every 4-output group of every policy role's Dense and of the value hidden Dense
+// is one thread's work, all in flight together -- a thread loads one float4 of 4 consecutive outputs
+// per k from the padded [K][N4] weights (gz_nn.hip) and keeps each output's sum in the k order of
+// dense_heads_seq, so the results are the same bit for bit -- instead of one Dense after another with
+// a barrier and a softmax between them (the weight loads are L2-latency bound); (B) one wave per
+// (role, board) softmax and per board's value output.  lg: per board a row of kp.lgrow floats,
+// [P4_0 | P4_1 | .. | VH4] (the policy sections absent with gemm_heads).
+template <int BPW, int NT>
+__device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, float* lg, int board0, int nb) {
+    static_assert(BPW >= 1 && BPW <= 4, "one softmax wave per board");
+    if (kp.gemm_heads && kp.maxP > kGemmSoftmaxMax) {
+        dense_heads_seq<BPW, NT>(kp, fk, lg, board0, nb);
+        return;
+    }
+    const int NPOS = kp.npos, R = kp.R, LG = kp.lgrow;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool gem = kp.gemm_heads != 0;
+    int pgroups = 0;
+    if (!gem)
+        for (int r = 0; r < R; ++r) pgroups += (kp.P[r] + 3) >> 2;
+    const int VH4 = (kp.VH + 3) & ~3;
+    const int voff = 4 * pgroups;                 // the value section's offset in a board's row
+    const int units = pgroups + (VH4 >> 2);
+    for (int u = tid; u < units; u += NT) {
+        const float* W;
+        const float* f;
+        int K, N4, q, off, r = 0;
+        if (u < pgroups) {
+            int uu = u;
+            off = 0;
+            for (; r < R - 1; ++r) {
+                const int g = (kp.P[r] + 3) >> 2;
+                if (uu < g) break;
+                uu -= g;
+                off += 4 * g;
+            }
+            q = uu;
+            W = kp.pd[r];
+            N4 = (kp.P[r] + 3) & ~3;
+            K = 2 * NPOS;
+            f = fk + (size_t)r * 2 * NPOS * BPW;
+        } else {
+            q = u - pgroups;
+            W = kp.vhw;
+            N4 = VH4;
+            K = kp.VK;
+            f = fk + (size_t)2 * R * NPOS * BPW;
+            off = voff;
+        }
+        float a[BPW][4];
+#pragma unroll
+        for (int b = 0; b < BPW; ++b) a[b][0] = a[b][1] = a[b][2] = a[b][3] = 0.f;
+        const float4* w4 = (const float4*)W + q;
+        const int rs = N4 >> 2;
+#pragma unroll 16   // many weight loads in flight: the loop is L2-latency bound
+        for (int k = 0; k < K; ++k) {
+            const float4 w = w4[(size_t)k * rs];
+#pragma unroll
+            for (int b = 0; b < BPW; ++b) {
+                const float x = f[k * BPW + b];
+                a[b][0] += x * w.x;
+                a[b][1] += x * w.y;
+                a[b][2] += x * w.z;
+                a[b][3] += x * w.w;
+            }
+        }
+        if (u < pgroups) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = 4 * q + i;
+                if (j < kp.P[r]) {
+                    const float bj = kp.pb[r][j];
+#pragma unroll
+                    for (int b = 0; b < BPW; ++b) lg[b * LG + off + j] = a[b][i] + bj;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = 4 * q + i;
+                if (j < kp.VH) {
+                    const float bj = kp.vhb[j];
+#pragma unroll
+                    for (int b = 0; b < BPW; ++b) lg[b * LG + off + j] = act_fn(a[b][i] + bj, kp.leaky);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const int ntask = R * nb + nb;
+    for (int t = wave; t < ntask; t += NT / 64) {
+        if (t < R * nb) {   // softmax of role r, board b
+            const int r = t / nb, b = t - r * nb, P = kp.P[r];
+            int lof = 0;
+            for (int q = 0; q < r; ++q) lof += gem ? kp.P[q] : ((kp.P[q] + 3) & ~3);
+            const int board = board0 + b;
+            const int sg = find_segment(kp, board);
+            float* out = kp.seg[sg].pol[r] + (size_t)(board - kp.seg[sg].row0) * P;
+            if (gem) {   // logits from policy_gemm_kernel (bias included), straight into registers
+                constexpr int NV = kGemmSoftmaxMax / 64;
+                const float* l = kp.glog + (size_t)board * kp.plog + lof;
+                float v[NV];
+#pragma unroll
+                for (int i = 0; i < NV; ++i) v[i] = lane + 64 * i < P ? l[lane + 64 * i] : -3.0e38f;
+                float m = -3.0e38f;
+#pragma unroll
+                for (int i = 0; i < NV; ++i) m = fmaxf(m, v[i]);
+                m = wave_max(m);
+                float sum = 0.f;
+#pragma unroll
+                for (int i = 0; i < NV; ++i)
+                    if (lane + 64 * i < P) sum += __expf(v[i] - m);
+                sum = wave_sum(sum);
+                const float inv = 1.f / sum;
+#pragma unroll
+                for (int i = 0; i < NV; ++i)
+                    if (lane + 64 * i < P) out[lane + 64 * i] = kp.logits ? v[i] : __expf(v[i] - m) * inv;
+            } else {
+                const float* l = lg + b * LG + lof;
+                float m = -3.0e38f;
+                for (int j = lane; j < P; j += 64) m = fmaxf(m, l[j]);
+                m = wave_max(m);
+                float sum = 0.f;
+                for (int j = lane; j < P; j += 64) sum += __expf(l[j] - m);
+                sum = wave_sum(sum);
+                const float inv = 1.f / sum;
+                if (kp.logits) {
+                    for (int j = lane; j < P; j += 64) out[j] = l[j];
+                } else {
+                    for (int j = lane; j < P; j += 64) out[j] = __expf(l[j] - m) * inv;
+                }
+            }
+        } else {            // value output of board b
+            const int b = t - R * nb;
+            const float* hv = lg + b * LG + voff;
+            float o[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int v = 0; v < kp.V; ++v) {
+                float sum = 0.f;
+                for (int k = lane; k < kp.VH; k += 64) sum += hv[k] * kp.vdw[(size_t)k * kp.V + v];
+                o[v] = wave_sum(sum) + kp.vdb[v];
+            }
+            if (lane == 0) {
+                const int board = board0 + b;
+                const int sg = find_segment(kp, board);
+                float* out = kp.seg[sg].val + (size_t)(board - kp.seg[sg].row0) * kp.V;
+                if (kp.logits) {
+                    for (int v = 0; v < kp.V; ++v) out[v] = o[v];
+                } else if (kp.value_sigmoid) {
+                    for (int v = 0; v < kp.V; ++v) out[v] = 1.f / (1.f + __expf(-o[v]));
+                } else {
+                    float m = o[0];
+                    for (int v = 1; v < kp.V; ++v) m = fmaxf(m, o[v]);
+                    float e[4], esum = 0.f;
+                    for (int v = 0; v < kp.V; ++v) { e[v] = __expf(o[v] - m); esum += e[v]; }
+                    for (int v = 0; v < kp.V; ++v) out[v] = e[v] / esum;
+                }
+            }
+        }
+    }
+}
+
+// floats per board of the dense heads' LDS outputs: the sequential path's max(P, VH) or the
+// two-phase path's [P4_0 | .. | VH4] row
+__host__ __device__ inline int heads_row(int R, const int* P, int VH) {
+    int maxP = 0, sum4 = 0;
+    for (int r = 0; r < R; ++r) {
+        maxP = P[r] > maxP ? P[r] : maxP;
+        sum4 += (P[r] + 3) & ~3;
+    }
+    int row = maxP > VH ? maxP : VH;
+    const int two = sum4 + ((VH + 3) & ~3);
+    return two > row ? two : row;
+}
+
 // LDS of the fused heads (trunk kernels with two activation images): 1x1-conv partials, features,
-// dense outputs
-__host__ __device__ inline int fused_heads_bytes(int npos, int R, int maxP, int VH, int gapF, int nb) {
+// dense outputs (lgrow = heads_row)
+__host__ __device__ inline int fused_heads_bytes(int npos, int R, int lgrow, int gapF, int nb) {
     const int FS = (2 * R + 1) * npos + gapF;   // (concat_all_layers nets never fuse the heads)
-    const int LMAX = maxP > VH ? maxP : VH;
-    return align16(4 * (2 * R + 1) * npos * 4) + align16(FS * nb * 4) + align16(nb * LMAX * 4);
+    return align16(4 * (2 * R + 1) * npos * 4) + align16(FS * nb * 4) + align16(nb * lgrow * 4);
 }
 
 // Separate heads launch (single-image trunk kernels: kHeadBoards boards per workgroup of features
@@ -1666,9 +1855,8 @@ __global__ void __launch_bounds__(256) heads_kernel(const KParams kp) {
 
 #endif
 
-__host__ inline int heads_lds_bytes(int FS, int maxP, int VH) {
-    const int LMAX = maxP > VH ? maxP : VH;
-    return (FS * kHeadBoards + kHeadBoards * LMAX + kHeadBoards * 4) * 4;
+__host__ inline int heads_lds_bytes(int FS, int lgrow) {
+    return (FS * kHeadBoards + kHeadBoards * lgrow + kHeadBoards * 4) * 4;
 }
 
 }  // namespace gznn

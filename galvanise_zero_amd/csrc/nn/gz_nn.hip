@@ -178,8 +178,10 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         const int kk0 = initial_kernel(d);
         const int k0p = ((kk0 * kk0 * d.input_channels + 31) / 32) * 32;
         const int p2 = precision == GZ_PRECISION_SPLIT ? 2 : 1;
+        (void)mp;
         return trunk_scratch_bytes(np, d.input_channels, k0p, d.role_count, p2) <= c.act_bytes &&
-               fused_heads_bytes(np, d.role_count, mp, d.value_hidden_size, gap_features(d), c.nb) <= c.act_bytes;
+               fused_heads_bytes(np, d.role_count, heads_row(d.role_count, d.policy_dist_count, d.value_hidden_size),
+                                 gap_features(d), c.nb) <= c.act_bytes;
     };
     if (kl.fn && !wg_fits(kl)) kl = KernelChoice{};
     if (kc.fn && !wg_fits(kc)) kc = KernelChoice{};
@@ -205,6 +207,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     int maxP = 0;
     for (int r = 0; r < d.role_count; ++r) maxP = std::max(maxP, d.policy_dist_count[r]);
     const int npos = d.input_columns * d.input_rows;
+    const int lgrow = heads_row(d.role_count, d.policy_dist_count, d.value_hidden_size);
     // LDS: two ping-pong activation images per board; the scratch (input staging, heads) aliases
     // the second image set, which holds nothing live at those times.
     const int scr_in = trunk_scratch_bytes(npos, d.input_channels, net->K0, d.role_count, net->p2);
@@ -215,8 +218,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         t.threads = c.threads;
         t.name = c.name;
         t.fused_heads = !c.single_image && !d.concat_all_layers;
-        const int scr = t.fused_heads ? std::max(scr_in, fused_heads_bytes(npos, d.role_count, maxP, d.value_hidden_size,
-                                                                           gap_features(d), c.nb))
+        const int scr = t.fused_heads ? std::max(scr_in, fused_heads_bytes(npos, d.role_count, lgrow, gap_features(d), c.nb))
                                       : scr_in;
         t.btab_off = c.single_image ? align16(std::max(c.act_bytes, scr))
                                     : c.nb * c.act_bytes + std::max(c.nb * c.act_bytes, scr);
@@ -231,7 +233,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     net->small = trunk(kc);
     net->large = trunk(kl);
     const int FS = 2 * d.role_count * npos + value_features(d);   // head features per board
-    net->heads_smem = heads_lds_bytes(FS, maxP, d.value_hidden_size);
+    net->heads_smem = heads_lds_bytes(FS, lgrow);
     // Large policies on nets whose every launch runs the separate heads kernel: the policy Dense
     // layers run as one MFMA GEMM per launch (policy_gemm_kernel) instead of heads_kernel's
     // per-4-board fp32 loop (amazons P = 3041: 12 % of the forward).  Every launch of such a net
@@ -258,6 +260,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     kp.cal = cal_layers(d);
     kp.nofuse = d.concat_all_layers ? 1 : 0;
     kp.maxP = maxP;
+    kp.lgrow = lgrow;
     kp.npos = npos;
     kp.gemm_heads = net->gemm_heads ? 1 : 0;
     kp.pkt = (2 * npos + 31) / 32;
@@ -500,6 +503,18 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     const float* vdb = cur.take(d.num_values);
     if ((size_t)(cur.p - blob) != count) return fail("internal: blob cursor mismatch");
 
+    // the dense heads' weights with their output dimension padded to a multiple of 4 ([K][N4], zero
+    // columns: forward_kernel.h dense_heads loads 4 consecutive outputs per float4)
+    auto pad4 = [](const float* w, int K, int N) {
+        const int N4 = (N + 3) & ~3;
+        std::vector<float> q((size_t)K * N4, 0.f);
+        for (int k = 0; k < K; ++k) std::memcpy(q.data() + (size_t)k * N4, w + (size_t)k * N, (size_t)N * 4);
+        return q;
+    };
+    std::vector<std::vector<float>> pdq(R);
+    for (int r = 0; r < R; ++r) pdq[r] = pad4(pdense[r], 2 * HW, d.policy_dist_count[r]);
+    const std::vector<float> vhq = pad4(vhw, VK, d.value_hidden_size);
+
     // device layout
     Layout L;
     const size_t o_w0 = L.alloc(w0.size() * 2), o_w0lo = L.alloc(std::max<size_t>(w0lo.size(), 1) * 2);
@@ -509,10 +524,10 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     const size_t o_wcl = L.alloc(wcl.size() * 4), o_bcl = L.alloc(bcl.size() * 4);
     size_t o_pd[GZ_MAX_ROLES], o_pb[GZ_MAX_ROLES];
     for (int r = 0; r < R; ++r) {
-        o_pd[r] = L.alloc((size_t)2 * HW * d.policy_dist_count[r] * 4);
+        o_pd[r] = L.alloc(pdq[r].size() * 4);
         o_pb[r] = L.alloc((size_t)d.policy_dist_count[r] * 4);
     }
-    const size_t o_vhw = L.alloc((size_t)VK * d.value_hidden_size * 4), o_vhb = L.alloc(d.value_hidden_size * 4);
+    const size_t o_vhw = L.alloc(vhq.size() * 4), o_vhb = L.alloc(d.value_hidden_size * 4);
     const size_t o_pre = L.alloc(pre.size() * 4), o_sew1 = L.alloc(sew1.size() * 4), o_sew2 = L.alloc(sew2.size() * 4);
     const size_t o_vdw = L.alloc((size_t)d.value_hidden_size * d.num_values * 4), o_vdb = L.alloc(d.num_values * 4);
     // policy_gemm_kernel's A fragments: W^T tiles [jt][kt][hi | lo][64 lanes][8 k] bf16, lane l holding
@@ -551,11 +566,10 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     put(o_wcl, wcl.data(), wcl.size() * 4);
     put(o_bcl, bcl.data(), bcl.size() * 4);
     for (int r = 0; r < R; ++r) {
-        // Keras layout [2HW][P_r] (k-major): heads_kernel reads one k row coalesced across outputs
-        put(o_pd[r], pdense[r], (size_t)2 * HW * d.policy_dist_count[r] * 4);
+        put(o_pd[r], pdq[r].data(), pdq[r].size() * 4);   // Keras [2HW][P_r] (k-major), rows padded to P4
         put(o_pb[r], pbias[r], (size_t)d.policy_dist_count[r] * 4);
     }
-    put(o_vhw, vhw, (size_t)VK * d.value_hidden_size * 4);   // Keras layout [VK][VH]
+    put(o_vhw, vhq.data(), vhq.size() * 4);   // Keras [VK][VH], rows padded to VH4
     put(o_pre, pre.data(), pre.size() * 4);
     put(o_sew1, sew1.data(), sew1.size() * 4);
     put(o_sew2, sew2.data(), sew2.size() * 4);
