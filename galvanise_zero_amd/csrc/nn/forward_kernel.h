@@ -87,6 +87,7 @@ struct KParams {
     unsigned long long* stamps;   // diagnostics only (GZ_KERNEL_STAMPS): [grid][8] s_memtime per phase
     int C, K0, B, R, VH, V, leaky, flatten_nchw, maxP, npos;
     int lgrow;               // floats per board of the dense heads' LDS outputs (heads_row)
+    int heads_seq;           // dense heads one Dense after another (the two-phase row does not fit the LDS)
     int H, W, wmagic;        // board rows / columns; wmagic = ceil(65536 / W) (Board::div)
     int value_sigmoid;       // legacy model files: independent sigmoid per value output
     int logits;              // diagnostics (gz_net_set_output_logits): write pre-softmax / pre-sigmoid outputs
@@ -1303,7 +1304,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     // of the last epilogue's output is in acc);
     // features in the model's Flatten order go to the scratch for heads_kernel ----------------
     const int HC = 2 * kp.R + (kp.cal ? 0 : 1);   // (concat_all_layers: the value features are written)
-    float* hpart = (float*)SCR;                                  // [4][HC][NPOS]
+    float* hpart = (float*)SCR;                                  // [NB][4][HC][NPOS]
     // the heads' 1x1 conv weights of this wave's channels, loaded together once for the NB boards
     // (two-role games, F <= 128) instead of one dependent global load per conv and board
     constexpr int kHoistHC = 5;
@@ -1325,7 +1326,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     constexpr bool FUSE = !SI;
     const bool fuse = FUSE && !kp.nofuse;   // nofuse: the features go to the device scratch
     constexpr int NBW = NB * WG;     // boards per workgroup
-    float* fk = (float*)(SCR0 + align16(4 * HC * NPOS * 4));
+    float* fk = (float*)(SCR0 + align16(NB * 4 * HC * NPOS * 4));
     float* lg = fk + align16(kp.FS * NBW * 4) / 4;
     // feature k of board bb
     auto feat_at = [&](int bb, int k) -> float& {
@@ -1363,7 +1364,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                 s += __shfl_xor(s, 16, 64);
                 s += __shfl_xor(s, 32, 64);
                 const int p = 16 * pt + li;
-                if (g == 0 && p < NPOS) hpart[(wave * HC + h) * NPOS + p] = s;
+                if (g == 0 && p < NPOS) hpart[((bb * 4 + wave) * HC + h) * NPOS + p] = s;
             }
         };
         if constexpr (HOIST_WH) {
@@ -1381,25 +1382,26 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                 head_conv(h, wv);
             }
         }
-        __syncthreads();
-        if (board < kp.n) {
-            for (int i = tid; i < HC * NPOS; i += kThreads) {
-                const int h = i / NPOS, p = i - (i / NPOS) * NPOS;
-                float s = kp.bh[h];
-#pragma unroll
-                for (int w = 0; w < 4; ++w) s += hpart[(w * HC + h) * NPOS + p];
-                s = act_fn(s, kp.leaky);
-                if (h < 2 * kp.R) {
-                    const int r = h >> 1, c = h & 1;
-                    const int idx = kp.flatten_nchw ? c * NPOS + p : p * 2 + c;
-                    feat_at(bb, r * 2 * NPOS + idx) = s;
-                } else {
-                    feat_at(bb, 2 * kp.R * NPOS + kp.gapF + p) = s;
-                }
-            }
-        }
-        __syncthreads();    // hpart is reused by the next board
     }
+    // every board's partials summed in one pass (one barrier pair for the NB boards)
+    __syncthreads();
+    for (int i = tid; i < NB * HC * NPOS; i += kThreads) {
+        const int bb = i / (HC * NPOS), hp = i - bb * (HC * NPOS);
+        const int h = hp / NPOS, p = hp - h * NPOS;
+        if (board0 + bb >= kp.n) continue;
+        float s = kp.bh[h];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) s += hpart[((bb * 4 + w) * HC + h) * NPOS + p];
+        s = act_fn(s, kp.leaky);
+        if (h < 2 * kp.R) {
+            const int r = h >> 1, c = h & 1;
+            const int idx = kp.flatten_nchw ? c * NPOS + p : p * 2 + c;
+            feat_at(bb, r * 2 * NPOS + idx) = s;
+        } else {
+            feat_at(bb, 2 * kp.R * NPOS + kp.gapF + p) = s;
+        }
+    }
+    __syncthreads();
     GZ_STAMP(3);
     if (fuse) {
         const int wb0 = blockIdx.x * NBW;
@@ -1591,7 +1593,7 @@ __device__ __forceinline__ void dense_heads_seq(const KParams& kp, const float* 
 template <int BPW, int NT>
 __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, float* lg, int board0, int nb) {
     static_assert(BPW >= 1 && BPW <= 4, "one softmax wave per board");
-    if (kp.gemm_heads && kp.maxP > kGemmSoftmaxMax) {
+    if (kp.heads_seq || (kp.gemm_heads && kp.maxP > kGemmSoftmaxMax)) {
         dense_heads_seq<BPW, NT>(kp, fk, lg, board0, nb);
         return;
     }
@@ -1742,24 +1744,25 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
     }
 }
 
-// floats per board of the dense heads' LDS outputs: the sequential path's max(P, VH) or the
-// two-phase path's [P4_0 | .. | VH4] row
-__host__ __device__ inline int heads_row(int R, const int* P, int VH) {
+// floats per board of the dense heads' LDS outputs: the sequential path's max(P, VH) (two = false)
+// or the two-phase path's [P4_0 | .. | VH4] row (two = true; at least the former)
+__host__ __device__ inline int heads_row(int R, const int* P, int VH, bool two = true) {
     int maxP = 0, sum4 = 0;
     for (int r = 0; r < R; ++r) {
         maxP = P[r] > maxP ? P[r] : maxP;
         sum4 += (P[r] + 3) & ~3;
     }
-    int row = maxP > VH ? maxP : VH;
-    const int two = sum4 + ((VH + 3) & ~3);
-    return two > row ? two : row;
+    const int row = maxP > VH ? maxP : VH;
+    const int tw = sum4 + ((VH + 3) & ~3);
+    return two && tw > row ? tw : row;
 }
 
 // LDS of the fused heads (trunk kernels with two activation images): 1x1-conv partials, features,
 // dense outputs (lgrow = heads_row)
-__host__ __device__ inline int fused_heads_bytes(int npos, int R, int lgrow, int gapF, int nb) {
+// (nb boards per workgroup, nbg of them per wave group: the 1x1-conv partials are per group)
+__host__ __device__ inline int fused_heads_bytes(int npos, int R, int lgrow, int gapF, int nb, int nbg) {
     const int FS = (2 * R + 1) * npos + gapF;   // (concat_all_layers nets never fuse the heads)
-    return align16(4 * (2 * R + 1) * npos * 4) + align16(FS * nb * 4) + align16(nb * lgrow * 4);
+    return align16(nbg * 4 * (2 * R + 1) * npos * 4) + align16(FS * nb * 4) + align16(nb * lgrow * 4);
 }
 
 // Separate heads launch (single-image trunk kernels: kHeadBoards boards per workgroup of features

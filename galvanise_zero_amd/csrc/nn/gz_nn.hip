@@ -181,7 +181,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         (void)mp;
         return trunk_scratch_bytes(np, d.input_channels, k0p, d.role_count, p2) <= c.act_bytes &&
                fused_heads_bytes(np, d.role_count, heads_row(d.role_count, d.policy_dist_count, d.value_hidden_size),
-                                 gap_features(d), c.nb) <= c.act_bytes;
+                                 gap_features(d), c.nb, 1) <= c.act_bytes;
     };
     if (kl.fn && !wg_fits(kl)) kl = KernelChoice{};
     if (kc.fn && !wg_fits(kc)) kc = KernelChoice{};
@@ -207,7 +207,10 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     int maxP = 0;
     for (int r = 0; r < d.role_count; ++r) maxP = std::max(maxP, d.policy_dist_count[r]);
     const int npos = d.input_columns * d.input_rows;
-    const int lgrow = heads_row(d.role_count, d.policy_dist_count, d.value_hidden_size);
+    // the dense heads' LDS row: the two-phase layout where every kernel's LDS still fits, else the
+    // sequential one (forward_kernel.h dense_heads / dense_heads_seq)
+    int lgrow = heads_row(d.role_count, d.policy_dist_count, d.value_hidden_size, true);
+    bool heads_seq = false;
     // LDS: two ping-pong activation images per board; the scratch (input staging, heads) aliases
     // the second image set, which holds nothing live at those times.
     const int scr_in = trunk_scratch_bytes(npos, d.input_channels, net->K0, d.role_count, net->p2);
@@ -218,7 +221,8 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         t.threads = c.threads;
         t.name = c.name;
         t.fused_heads = !c.single_image && !d.concat_all_layers;
-        const int scr = t.fused_heads ? std::max(scr_in, fused_heads_bytes(npos, d.role_count, lgrow, gap_features(d), c.nb))
+        const int scr = t.fused_heads ? std::max(scr_in, fused_heads_bytes(npos, d.role_count, lgrow, gap_features(d), c.nb,
+                                                                           c.threads == 512 ? 1 : c.nb))
                                       : scr_in;
         t.btab_off = c.single_image ? align16(std::max(c.act_bytes, scr))
                                     : c.nb * c.act_bytes + std::max(c.nb * c.act_bytes, scr);
@@ -230,10 +234,16 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         if (d.concat_all_layers) t.smem += align16(4 * c.nb * npos * 4);
         return t;
     };
-    net->small = trunk(kc);
-    net->large = trunk(kl);
     const int FS = 2 * d.role_count * npos + value_features(d);   // head features per board
-    net->heads_smem = heads_lds_bytes(FS, lgrow);
+    for (int pass = 0; pass < 2; ++pass) {
+        net->small = trunk(kc);
+        net->large = trunk(kl);
+        net->heads_smem = heads_lds_bytes(FS, lgrow);
+        if (pass == 1 || (net->small.smem <= 160 * 1024 && net->large.smem <= 160 * 1024 && net->heads_smem <= 160 * 1024))
+            break;
+        heads_seq = true;
+        lgrow = heads_row(d.role_count, d.policy_dist_count, d.value_hidden_size, false);
+    }
     // Large policies on nets whose every launch runs the separate heads kernel: the policy Dense
     // layers run as one MFMA GEMM per launch (policy_gemm_kernel) instead of heads_kernel's
     // per-4-board fp32 loop (amazons P = 3041: 12 % of the forward).  Every launch of such a net
@@ -261,6 +271,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     kp.nofuse = d.concat_all_layers ? 1 : 0;
     kp.maxP = maxP;
     kp.lgrow = lgrow;
+    kp.heads_seq = heads_seq ? 1 : 0;
     kp.npos = npos;
     kp.gemm_heads = net->gemm_heads ? 1 : 0;
     kp.pkt = (2 * npos + 31) / 32;
