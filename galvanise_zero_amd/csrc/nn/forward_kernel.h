@@ -141,6 +141,10 @@ struct Board {
 // slower than their fully unrolled conv on MI355X (cfg4 12.9 -> 14.6 ms, cfg5 equal at 1,024 rows,
 // bit-identical; profiles/r04e_kexp.txt), so off; kept for experiments (tools/kexp siloop)
 constexpr bool kLoopSI = false;
+// Two-pass split (P = 2): the epilogues write each value's lo parts straight to the workgroup's lo
+// scratch and its hi parts into the image, in one pass (instead of lo parts into the image, a
+// copy-out sweep, then the hi parts)
+constexpr bool kLoDirect = true;
 
 // ring depth: largest R dividing the stages per conv with R slots of KS*CT fragments <= cap VGPRs
 __host__ __device__ constexpr int ring_depth(int nst, int ks, int ct, int cap) {
@@ -314,6 +318,20 @@ __device__ __forceinline__ void store_act(char* X, int p, int co, f32x4 v, int n
             l.y = pack2(bf16_lo(v[2]), bf16_lo(v[3]));
             *(uint2*)(a + G::HALF) = l;
         }
+    }
+}
+
+// P = 2 (kLoDirect): the lo parts of v straight to the workgroup's lo scratch, at the byte offset
+// the image would hold them (on-board positions only)
+template <int F, int PTN>
+__device__ __forceinline__ void store_lo_scratch(char* xlo, int p, int co, f32x4 v, int npos) {
+    using G = Geo<F, PTN, 1, 2>;
+    if (p < npos) {
+        const int chunk = (co >> 3) + swz(p);
+        uint2 l;
+        l.x = pack2(bf16_lo(v[0]), bf16_lo(v[1]));
+        l.y = pack2(bf16_lo(v[2]), bf16_lo(v[3]));
+        *(uint2*)(xlo + p * G::ROWS + (chunk << 4) + (co & 7) * 2) = l;
     }
 }
 
@@ -1093,13 +1111,18 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                 if constexpr (RG) rg0[(ct * TT + bb * PT + pt) * 64] = v;
                 else resid[ct][bb * PT + pt] = v;
                 acc[ct][bb * PT + pt] = v;    // the heads read acc when there is no residual block
-                store_act<F, PTN, P, !G::SI>(X0 + bb * ACT, 16 * pt + li, co, preact ? pre_act(v, psc, psh, kp.leaky) : v, NPOS);
+                if constexpr (P == 2 && kLoDirect) {
+                    store_act<F, PTN, 1, false>(X0 + bb * ACT, 16 * pt + li, co, v, NPOS);
+                    store_lo_scratch<F, PTN>(xlo, 16 * pt + li, co, v, NPOS);
+                } else {
+                    store_act<F, PTN, P, !G::SI>(X0 + bb * ACT, 16 * pt + li, co, preact ? pre_act(v, psc, psh, kp.leaky) : v, NPOS);
+                }
             }
         }
         if constexpr (V2)
             if (kp.cal) cal_partial(0, bb);   // layer 0: the initial conv block's output
         __syncthreads();    // scratch is reused by the next board
-        if constexpr (P == 2) save_lo_write_hi<F, PTN>(X0, xlo, acc, NPOS, tid, co_base, li, g);
+        if constexpr (P == 2 && !kLoDirect) save_lo_write_hi<F, PTN>(X0, xlo, acc, NPOS, tid, co_base, li, g);
     }
     for (int i = tid; i < NB * G::ZROWS * G::ROWS / 4; i += kThreads) {
         const int bb = i / (G::ZROWS * G::ROWS / 4), j = i % (G::ZROWS * G::ROWS / 4);
@@ -1136,6 +1159,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
             if constexpr (RG) launder_ptr(rgc);
             char* Xe = X0;
             launder_ptr(Xe);
+            char* xloe = xlo;
+            if constexpr (P == 2) launder_ptr(xloe);
             int lie = li, ge = g;    // (and their offsets: the lane's row and channel terms)
             launder(lie);
             launder(ge);
@@ -1200,12 +1225,18 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                         if constexpr (RG) rgc[(ct * TT + t) * 64] = v;
                         else resid[ct][t] = v;
                     }
-                    if (second || P == 2) acc[ct][t] = v;
-                    store_act<F, PTN, P, !G::SI>(Xe, 16 * t + lie, co, v, NPOS);
+                    if constexpr (P == 2 && kLoDirect) {
+                        if (second) acc[ct][t] = v;
+                        store_act<F, PTN, 1, false>(Xe, 16 * t + lie, co, v, NPOS);
+                        store_lo_scratch<F, PTN>(xloe, 16 * t + lie, co, v, NPOS);
+                    } else {
+                        if (second || P == 2) acc[ct][t] = v;
+                        store_act<F, PTN, P, !G::SI>(Xe, 16 * t + lie, co, v, NPOS);
+                    }
                 }
             }
             __syncthreads();
-            if constexpr (P == 2) save_lo_write_hi<F, PTN>(Xe, xlo, acc, NPOS, tid, co_base, lie, ge);
+            if constexpr (P == 2 && !kLoDirect) save_lo_write_hi<F, PTN>(Xe, xlo, acc, NPOS, tid, co_base, lie, ge);
         }
     } else
     for (int blk = 0; blk < kp.B; ++blk) {

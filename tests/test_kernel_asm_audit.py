@@ -1,6 +1,6 @@
 """The split kernels' inline-asm MFMA chains are hazard-free as compiled (tests/kernel_asm_audit.py):
 the auditor itself on synthetic assembly, then the gfx950 assembly of every trunk kernel that runs
-chains (hipcc -S of trunk_f128.hip / trunk_f128_v2.hip, CPU only; the F = 64 and 256 split
+chains (hipcc -S of one translation unit instantiating them, CPU only; the F = 64 and 256 split
 kernels run the unrolled conv with builtins)."""
 import os
 import shutil
@@ -60,17 +60,34 @@ def test_auditor_rule3_loop_copy():
     assert any("rule 3" in v for v in violations(body))
 
 
+# every trunk instantiation that runs the split looped conv (the F = 128 split kernels, v1 and v2,
+# one and two boards, the two-group kernel), in one translation unit
+AUDIT_TU = """#include "trunk_variants.h"
+namespace gznn {
+template __global__ void trunk_kernel<128, 2, 1, 1, 3>(KParams);
+template __global__ void trunk_kernel<128, 2, 2, 1, 3>(KParams);
+template __global__ void trunk_kernel<128, 3, 1, 1, 3>(KParams);
+template __global__ void trunk_kernel<128, 3, 2, 1, 3>(KParams);
+template __global__ void trunk_kernel<128, 4, 1, 1, 3>(KParams);
+template __global__ void trunk_kernel<128, 4, 2, 1, 3>(KParams);
+template __global__ void trunk_kernel_v2<128, 4, 1, 1, 3>(KParams);
+template __global__ void trunk_kernel_v2<128, 4, 2, 1, 3>(KParams);
+template __global__ void trunk_kernel8<128, 4, 3>(KParams);
+}
+"""
+
+
 @pytest.mark.skipif(shutil.which(HIPCC) is None and not os.path.exists(HIPCC), reason="hipcc absent")
-@pytest.mark.parametrize("tu", ["trunk_f128.hip", "trunk_f128_v2.hip"])
-def test_compiled_chains_hazard_free(tu, tmp_path):
-    out = tmp_path / (tu + ".s")
+def test_compiled_chains_hazard_free(tmp_path):
+    src = tmp_path / "audit_tu.hip"
+    src.write_text(AUDIT_TU)
+    out = tmp_path / "audit_tu.s"
     subprocess.check_call([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-parameter",
-                           "--cuda-device-only", "-S", "-o", str(out), os.path.join(NN, tu)],
+                           "--cuda-device-only", "-S", "-I", NN, "-o", str(out), str(src)],
                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     res = kaa.audit(out.read_text())
-    assert res, "no kernel with asm MFMA chains in %s" % tu
+    assert len(res) == 9, sorted(res)     # every instantiation above runs chains
     for name, (n, bad) in res.items():
         assert n > 0
         assert bad == [], (name, bad[:5])
-    if tu == "trunk_f128.hip":   # the headline kernel runs chains
-        assert any("ILi128ELi4ELi2ELi1ELi3E" in k for k in res)
+    assert any("ILi128ELi4ELi2ELi1ELi3E" in k for k in res)   # the headline kernel
