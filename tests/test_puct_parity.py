@@ -195,13 +195,17 @@ def test_spin_fast_path_identical():
     outs = []
     # GZ_SPIN_FAST=2: the fast path without the register-resident runs (evaluator.cpp spinRunRegs)
     # GZ_SPIN_VEC=1: the AVX2 register loops instead of the scalar ones (evaluator.cpp spin_wins_v)
+    # (the five runs are independent processes: run side by side)
+    procs = []
     for env in ({"GZ_SPIN_FAST": "0"}, {"GZ_SPIN_FAST": "1"}, {"GZ_SPIN_FAST": "2"},
                 {"GZ_SPIN_FAST": "1", "GZ_VERIFY_FASTPATH": "1"}, {"GZ_SPIN_FAST": "1", "GZ_SPIN_VEC": "1"}):
         e = dict(os.environ, **env)
-        r = subprocess.run([sys.executable, script, "breakthrough", "16", "3000", "100"], env=e,
-                           capture_output=True, text=True, timeout=600)
-        assert r.returncode == 0, r.stderr[-2000:]
-        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+        procs.append(subprocess.Popen([sys.executable, script, "breakthrough", "16", "3000", "100"], env=e,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    for pr in procs:
+        out, err = pr.communicate(timeout=600)
+        assert pr.returncode == 0, err[-2000:]
+        outs.append(json.loads(out.strip().splitlines()[-1]))
     assert outs[0] == outs[1] == outs[2] == outs[3] == outs[4]
     assert outs[0]["samples"] > 50 and outs[0]["tree_playouts"] > 3 * outs[0]["evaluations"]
 
