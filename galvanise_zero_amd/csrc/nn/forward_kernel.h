@@ -166,7 +166,9 @@ __host__ __device__ constexpr int lcm_c(int a, int b) { return a / gcd_c(a, b) *
 // in from a per-workgroup device scratch (written by the previous epilogue) and pass 1 adds
 // W_hi x_lo.
 // WG = wave groups per workgroup: 1 (4 waves for NB boards) or 2 (8 waves, 2 per SIMD: group g takes
-// board g of the workgroup with NB = 1; the register budget is then 256 per wave)
+// board g of the workgroup with NB = 1; the register budget is then 256 per wave); WG = 3: ONE group
+// of 8 waves for the NB boards, each wave a half of the 4-wave layout's output channels (CT halves:
+// the same weight stream per workgroup, two waves per SIMD, 256 registers per wave)
 template <int F, int PTN, int NB = 1, int P = 1, int WG = 1>
 struct Geo {
     static constexpr int P2 = P == 3 ? 2 : 1;        // bf16 parts per activation in the LDS image
@@ -175,7 +177,9 @@ struct Geo {
     static constexpr int NPOS = 16 * PTN;            // position capacity (the real count is kp.npos)
     static constexpr int PT = PTN;                   // position tiles per board (MFMA N)
     static constexpr int TT = NB * PT;               // position tiles per wave (all boards)
-    static constexpr int CT = F / 64;                // co tiles per wave (MFMA M)
+    static constexpr int NWV = WG == 3 ? 8 : 4;      // waves per group
+    static constexpr int NGR = WG == 2 ? 2 : 1;      // wave groups per workgroup
+    static constexpr int CT = F / (16 * NWV);        // co tiles per wave (MFMA M)
     static constexpr int KC = F / 32;                // k-steps per tap
     static constexpr int CPR = F / 8;                // 16-byte chunks of channels per row
     // Split precision with F = 128 (16 chunks, 256 B per part): the rotation wraps inside the
@@ -239,7 +243,7 @@ struct Geo {
     static constexpr bool TRACKED = SI || LIVE_VGPRS > 300 || (P2 == 2 && (NB == 2 || WG == 2));
     static_assert(F % 64 == 0, "filters must be a multiple of 64");
     static_assert(!SI || NB == 1, "single-image mode takes one board per workgroup");
-    static_assert(WG == 1 || (NB == 1 && !SI), "wave groups: one board per group, two images");
+    static_assert(WG == 1 || (WG == 2 && NB == 1 && !SI) || (WG == 3 && !SI && CT >= 1), "wave groups: two images");
     static_assert(!RG || SI, "the global residual is implemented for single-image kernels");
     static constexpr int RESID_BYTES = RG ? 4 * CT * TT * 64 * 16 : 0;   // per workgroup
     // P = 2: the lo image of each workgroup (device scratch after the grid's residual scratch)
@@ -266,10 +270,10 @@ __device__ __forceinline__ int swz(int q) { return (2 * q) & 14; }
 
 // LDS bytes of the trunk kernel beyond the two activation image sets: bias table + scratch
 // (input staging / 1x1-head partials; the scratch aliases the second image set).
-__host__ __device__ inline int trunk_scratch_bytes(int npos, int C, int K0, int R, int P2 = 1) {
+__host__ __device__ inline int trunk_scratch_bytes(int npos, int C, int K0, int R, int P2, int F) {
     const int in_stage = align16(C * npos * 4) + P2 * align16((npos + 1) * K0 * 2);
     const int hc = 2 * R + 1;
-    const int heads = align16(4 * hc * npos * 4);
+    const int heads = align16((F / 16) * hc * npos * 4);   // head-conv partials per 16-channel tile
     return in_stage > heads ? in_stage : heads;
 }
 __host__ __device__ inline int bias_table_bytes(int F, int B) { return align16((2 * B) * F * 4); }
@@ -459,8 +463,8 @@ __device__ __forceinline__ int tap_offset(const TapAddr& t, int kc) {
 // conv's first stage; on entry stages gs0 .. gs0+R-2 are in flight in ring slots 0..R-2.
 template <int F, int PTN, int NB, int P, int WG, int PASS, int ST>
 __device__ __forceinline__ void conv_stage(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
-                                           f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
-                                           bf16x8 (&b)[2][Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
+                                           f32x4 (&acc)[Geo<F, PTN, NB, P, WG>::CT][Geo<F, PTN, NB, P, WG>::TT],
+                                           bf16x8 (&b)[2][Geo<F, PTN, NB, P, WG>::TT][Geo<F, PTN, NB, P, WG>::P2],
                                            const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane,
                                            const Board& bd) {
     using G = Geo<F, PTN, NB, P, WG>;
@@ -537,8 +541,8 @@ __device__ __forceinline__ void ring_prime(Ring<F, PTN, NB, P, WG>& ring, const 
 
 template <int F, int PTN, int NB, int P, int WG, int PASS, int... ST>
 __device__ __forceinline__ void conv_stages(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
-                                            f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
-                                            bf16x8 (&b)[2][Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
+                                            f32x4 (&acc)[Geo<F, PTN, NB, P, WG>::CT][Geo<F, PTN, NB, P, WG>::TT],
+                                            bf16x8 (&b)[2][Geo<F, PTN, NB, P, WG>::TT][Geo<F, PTN, NB, P, WG>::P2],
                                             const __bf16* wres, uint32_t woff, int gs0, int gmax, int& lane,
                                             const Board& bd, std::integer_sequence<int, ST...>) {
     (conv_stage<F, PTN, NB, P, WG, PASS, ST>(X, ring, acc, b, wres, woff, gs0, gmax, lane, bd), ...);
@@ -547,7 +551,7 @@ __device__ __forceinline__ void conv_stages(const char* __restrict__ X, Ring<F, 
 // PASS (P = 2): 0 starts the accumulators, 1 adds to them
 template <int F, int PTN, int NB, int P, int WG = 1, int PASS = 0>
 __device__ __forceinline__ void conv3x3(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
-                                        f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
+                                        f32x4 (&acc)[Geo<F, PTN, NB, P, WG>::CT][Geo<F, PTN, NB, P, WG>::TT],
                                         const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane,
                                         const Board& bd) {
     using G = Geo<F, PTN, NB, P, WG>;
@@ -623,8 +627,8 @@ __device__ __forceinline__ void split_chain_leave(f32x4 (&acc)[CT][TT]) {
 
 template <int F, int PTN, int NB, int P, int WG, int PASS, int ST>
 __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
-                                             f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
-                                             bf16x8 (&b)[Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
+                                             f32x4 (&acc)[Geo<F, PTN, NB, P, WG>::CT][Geo<F, PTN, NB, P, WG>::TT],
+                                             bf16x8 (&b)[Geo<F, PTN, NB, P, WG>::TT][Geo<F, PTN, NB, P, WG>::P2],
                                              const __bf16* wres, uint32_t woff, int gs_it, int gmax, int& lane,
                                              const Board& bd, int tap0, bool last_it) {
     using G = Geo<F, PTN, NB, P, WG>;
@@ -693,8 +697,8 @@ __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F,
 
 template <int F, int PTN, int NB, int P, int WG, int PASS, int... ST>
 __device__ __forceinline__ void conv_iter(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
-                                          f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
-                                          bf16x8 (&b)[Geo<F, PTN, NB, P>::TT][Geo<F, PTN, NB, P>::P2],
+                                          f32x4 (&acc)[Geo<F, PTN, NB, P, WG>::CT][Geo<F, PTN, NB, P, WG>::TT],
+                                          bf16x8 (&b)[Geo<F, PTN, NB, P, WG>::TT][Geo<F, PTN, NB, P, WG>::P2],
                                           const __bf16* wres, uint32_t woff, int gs_it, int gmax, int& lane,
                                           const Board& bd, int tap0, bool last_it, std::integer_sequence<int, ST...>) {
     (conv_stage_l<F, PTN, NB, P, WG, PASS, ST>(X, ring, acc, b, wres, woff, gs_it, gmax, lane, bd, tap0, last_it), ...);
@@ -703,7 +707,7 @@ __device__ __forceinline__ void conv_iter(const char* __restrict__ X, Ring<F, PT
 // PASS (P = 2): 0 starts the accumulators, 1 adds to them
 template <int F, int PTN, int NB, int P, int WG = 1, int PASS = 0>
 __device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
-                                               f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
+                                               f32x4 (&acc)[Geo<F, PTN, NB, P, WG>::CT][Geo<F, PTN, NB, P, WG>::TT],
                                                const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane,
                                                const Board& bd) {
     using G = Geo<F, PTN, NB, P, WG>;
@@ -735,10 +739,10 @@ __device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<
 // Per-board channel sums over the board's positions of the wave's accumulator tiles: lane group g
 // (lanes 16g .. 16g+15) ends with the sums of channels co_base + 16ct + 4g + r in every lane.  The
 // order (tiles ascending, then a butterfly over the 16 lanes) depends only on the board.
-template <int F, int PTN, int NB, int P>
-__device__ __forceinline__ f32x4 board_channel_sum(const f32x4 (&acc)[Geo<F, PTN, NB, P>::CT][Geo<F, PTN, NB, P>::TT],
+template <int F, int PTN, int NB, int P, int WG = 1>
+__device__ __forceinline__ f32x4 board_channel_sum(const f32x4 (&acc)[Geo<F, PTN, NB, P, WG>::CT][Geo<F, PTN, NB, P, WG>::TT],
                                                    int ct, int bb, int li, int npos) {
-    using G = Geo<F, PTN, NB, P>;
+    using G = Geo<F, PTN, NB, P, WG>;
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int pt = 0; pt < G::PT; ++pt)
@@ -867,7 +871,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                   "split precision: F <= 128 (F = 256: single image)");
     constexpr int P2 = G::P2;
     constexpr int IP2 = G::WP;    // bf16 parts of the initial conv's operands (im2col scratch, w0 / w0lo)
-    constexpr int PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, kThreads = 256;
+    constexpr int PT = G::PT, TT = G::TT, CT = G::CT, R = G::R, NWV = G::NWV, NGR = G::NGR, kThreads = 64 * NWV;
     const int NPOS = kp.npos, H = kp.H, W = kp.W;     // the board (NPOS <= G::NPOS)
     Board bd{H, W, NPOS, kp.wmagic, {}};
     {
@@ -891,14 +895,14 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // wave group grp (WG = 2: threads 256 grp .. 256 grp + 255) takes boards NB grp .. of the
     // workgroup; LDS: image set 0 [WG][NB][ACT], image set 1 [WG][NB][ACT], bias table
-    const int grp = WG == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+    const int grp = NGR == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
     char* X0 = smem + grp * NB * ACT;                                  // [NB][ACT]
-    char* X1 = SI ? smem : smem + WG * NB * ACT + grp * NB * ACT;      // [NB][ACT]
+    char* X1 = SI ? smem : smem + NGR * NB * ACT + grp * NB * ACT;      // [NB][ACT]
     char* SCR = X1;                  // scratch aliases X1 while X1 holds no live activations
-    char* SCR0 = SI ? smem : smem + WG * NB * ACT;   // group 0's scratch (the fused heads' shared features)
+    char* SCR0 = SI ? smem : smem + NGR * NB * ACT;   // group 0's scratch (the fused heads' shared features)
     float* btab = (float*)(smem + kp.btab_off);   // trunk conv biases [2B][F], after X1 / scratch
 
-    const int board0 = (blockIdx.x * WG + grp) * NB;
+    const int board0 = (blockIdx.x * NGR + grp) * NB;
     const int tid = threadIdx.x & (kThreads - 1);   // within the group
 #define GZ_STAMP(i) \
     if (kp.stamps && threadIdx.x == 0) kp.stamps[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime()
@@ -906,7 +910,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, li = lane & 15;
-    const int co_base = wave * (F / 4);
+    const int co_base = wave * (F / NWV);
     const int C = kp.C, K0 = kp.K0;
 
     // The NB boards' input planes, fetched before anything else with 16-byte loads so that one round
@@ -983,7 +987,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         }
     };
 
-    for (int i = threadIdx.x; i < 2 * kp.B * F; i += kThreads * WG) btab[i] = kp.bres[i];
+    for (int i = threadIdx.x; i < 2 * kp.B * F; i += kThreads * NGR) btab[i] = kp.bres[i];
     for (int i = tid; i < NB * G::ZROWS * G::ROWS / 4; i += kThreads) {
         const int bb = i / (G::ZROWS * G::ROWS / 4), j = i % (G::ZROWS * G::ROWS / 4);
         ((uint32_t*)(X0 + bb * ACT + NPOS * G::ROWS))[j] = 0u;
@@ -1335,7 +1339,10 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     // of the last epilogue's output is in acc);
     // features in the model's Flatten order go to the scratch for heads_kernel ----------------
     const int HC = 2 * kp.R + (kp.cal ? 0 : 1);   // (concat_all_layers: the value features are written)
-    float* hpart = (float*)SCR;                                  // [NB][4][HC][NPOS]
+    // head-conv partials per 16-channel tile (the same sums whatever the waves' channel split, so
+    // every variant -- 4 or 8 waves -- computes every row identically)
+    constexpr int NT16 = F / 16;
+    float* hpart = (float*)SCR;                                  // [NB][NT16][HC][NPOS]
     // the heads' 1x1 conv weights of this wave's channels, loaded together once for the NB boards
     // (two-role games, F <= 128) instead of one dependent global load per conv and board
     constexpr int kHoistHC = 5;
@@ -1356,8 +1363,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     // in group 0's, after its partials)
     constexpr bool FUSE = !SI;
     const bool fuse = FUSE && !kp.nofuse;   // nofuse: the features go to the device scratch
-    constexpr int NBW = NB * WG;     // boards per workgroup
-    float* fk = (float*)(SCR0 + align16(NB * 4 * HC * NPOS * 4));
+    constexpr int NBW = NB * NGR;    // boards per workgroup
+    float* fk = (float*)(SCR0 + align16(NB * NT16 * HC * NPOS * 4));
     float* lg = fk + align16(kp.FS * NBW * 4) / 4;
     // feature k of board bb
     auto feat_at = [&](int bb, int k) -> float& {
@@ -1371,7 +1378,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
             const float inv = 1.f / (float)NPOS;
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
-                const f32x4 sm = board_channel_sum<F, PTN, NB, P>(acc, ct, bb, li, NPOS);
+                const f32x4 sm = board_channel_sum<F, PTN, NB, P, WG>(acc, ct, bb, li, NPOS);
                 const int co = co_base + 16 * ct + 4 * g;
                 if (li == 0)
 #pragma unroll
@@ -1383,19 +1390,18 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         auto head_conv = [&](int h, const float4 (&wv)[CT]) {
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt) {
-                float s = 0.f;
+                const int p = 16 * pt + li;
 #pragma unroll
                 for (int ct = 0; ct < CT; ++ct) {
                     const f32x4 a = acc[ct][bb * PT + pt];
-                    s += a[0] * wv[ct].x;
+                    float s = a[0] * wv[ct].x;
                     s += a[1] * wv[ct].y;
                     s += a[2] * wv[ct].z;
                     s += a[3] * wv[ct].w;
+                    s += __shfl_xor(s, 16, 64);
+                    s += __shfl_xor(s, 32, 64);
+                    if (g == 0 && p < NPOS) hpart[((bb * NT16 + co_base / 16 + ct) * HC + h) * NPOS + p] = s;
                 }
-                s += __shfl_xor(s, 16, 64);
-                s += __shfl_xor(s, 32, 64);
-                const int p = 16 * pt + li;
-                if (g == 0 && p < NPOS) hpart[((bb * 4 + wave) * HC + h) * NPOS + p] = s;
             }
         };
         if constexpr (HOIST_WH) {
@@ -1422,7 +1428,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         if (board0 + bb >= kp.n) continue;
         float s = kp.bh[h];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) s += hpart[((bb * 4 + w) * HC + h) * NPOS + p];
+        for (int w = 0; w < NT16; ++w) s += hpart[((bb * NT16 + w) * HC + h) * NPOS + p];
         s = act_fn(s, kp.leaky);
         if (h < 2 * kp.R) {
             const int r = h >> 1, c = h & 1;
@@ -1437,7 +1443,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     if (fuse) {
         const int wb0 = blockIdx.x * NBW;
         const int nb = kp.n - wb0 < NBW ? kp.n - wb0 : NBW;
-        dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);
+        dense_heads<NBW, kThreads * NGR>(kp, fk, lg, wb0, nb);
     }
     GZ_STAMP(4);
 #undef GZ_STAMP
@@ -1458,6 +1464,15 @@ template <int F, int PTN, int P>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 trunk_kernel8(const KParams kp) {
     trunk_body<F, PTN, 1, 2, P, false, 2>(kp);
+}
+
+// One group of 8 waves (two per SIMD) for two boards, each wave half of the 4-wave kernel's output
+// channels (variant 24): the weight stream per workgroup stays that of trunk_kernel<.., 2, ..>, the B
+// fragments are read by twice as many waves
+template <int F, int PTN, int P>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+trunk_kernel_w8(const KParams kp) {
+    trunk_body<F, PTN, 2, 2, P, false, 3>(kp);
 }
 
 template <int F, int PTN, int NB, int WPE, int P>
@@ -1790,10 +1805,11 @@ __host__ __device__ inline int heads_row(int R, const int* P, int VH, bool two =
 
 // LDS of the fused heads (trunk kernels with two activation images): 1x1-conv partials, features,
 // dense outputs (lgrow = heads_row)
-// (nb boards per workgroup, nbg of them per wave group: the 1x1-conv partials are per group)
-__host__ __device__ inline int fused_heads_bytes(int npos, int R, int lgrow, int gapF, int nb, int nbg) {
+// (nb boards per workgroup, nbg of them per wave group; F padded filters: the 1x1-conv partials are
+// per group, board and 16-channel tile)
+__host__ __device__ inline int fused_heads_bytes(int npos, int R, int lgrow, int gapF, int nb, int nbg, int F) {
     const int FS = (2 * R + 1) * npos + gapF;   // (concat_all_layers nets never fuse the heads)
-    return align16(nbg * 4 * (2 * R + 1) * npos * 4) + align16(FS * nb * 4) + align16(nb * lgrow * 4);
+    return align16(nbg * (F / 16) * (2 * R + 1) * npos * 4) + align16(FS * nb * 4) + align16(nb * lgrow * 4);
 }
 
 // Separate heads launch (single-image trunk kernels: kHeadBoards boards per workgroup of features

@@ -92,7 +92,9 @@ extern "C" const char* gz_nn_last_error(void) { return g_err.c_str(); }
 // choosing per launch keeps results batch-invariant.
 // Launches of 257-383 rows also take the two-board kernel: at one board per workgroup they would
 // need a second wave of workgroups on the 256 CUs (one trunk workgroup per CU by LDS).
-constexpr int kSmallVariant = 11, kLargeVariant = 21, kLargeMinRows = 257;
+// large launches: the 8-wave two-board kernel where compiled (F = 128 split v1 nets: 5 % faster than
+// 21 at the runner's 1,024-row launches, bit-identical; profiles/r04t_w8_kexp.txt), else 21
+constexpr int kSmallVariant = 11, kLargeVariant = 24, kLargeFallback = 21, kLargeMinRows = 257;
 constexpr int kCUs = 256;
 
 static KernelChoice select_kernel(int fpad, int pt, int v, int precision, bool v2) {
@@ -169,9 +171,10 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     const bool v2 = d.resnet_v2 != 0;
     KernelChoice kc = select_kernel(fpad, pt, vs, precision, v2);
     KernelChoice kl = select_kernel(fpad, pt, vl, precision, v2);
+    if (!kl.fn && vl == kLargeVariant) kl = select_kernel(fpad, pt, kLargeFallback, precision, v2);
     // wave-group kernels: each group's staging / heads scratch must fit its own image
     auto wg_fits = [&](const KernelChoice& c) {
-        if (c.threads == 256) return true;
+        if (c.groups == 1) return true;
         const int np = d.input_columns * d.input_rows;
         int mp = 0;
         for (int r = 0; r < d.role_count; ++r) mp = std::max(mp, d.policy_dist_count[r]);
@@ -179,9 +182,9 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         const int k0p = ((kk0 * kk0 * d.input_channels + 31) / 32) * 32;
         const int p2 = precision == GZ_PRECISION_SPLIT ? 2 : 1;
         (void)mp;
-        return trunk_scratch_bytes(np, d.input_channels, k0p, d.role_count, p2) <= c.act_bytes &&
+        return trunk_scratch_bytes(np, d.input_channels, k0p, d.role_count, p2, fpad) <= c.act_bytes &&
                fused_heads_bytes(np, d.role_count, heads_row(d.role_count, d.policy_dist_count, d.value_hidden_size),
-                                 gap_features(d), c.nb, 1) <= c.act_bytes;
+                                 gap_features(d), c.nb, 1, fpad) <= c.act_bytes;
     };
     if (kl.fn && !wg_fits(kl)) kl = KernelChoice{};
     if (kc.fn && !wg_fits(kc)) kc = KernelChoice{};
@@ -213,7 +216,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     bool heads_seq = false;
     // LDS: two ping-pong activation images per board; the scratch (input staging, heads) aliases
     // the second image set, which holds nothing live at those times.
-    const int scr_in = trunk_scratch_bytes(npos, d.input_channels, net->K0, d.role_count, net->p2);
+    const int scr_in = trunk_scratch_bytes(npos, d.input_channels, net->K0, d.role_count, net->p2, fpad);
     auto trunk = [&](const KernelChoice& c) {
         gz_net::Trunk t;
         t.fn = c.fn;
@@ -222,7 +225,7 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
         t.name = c.name;
         t.fused_heads = !c.single_image && !d.concat_all_layers;
         const int scr = t.fused_heads ? std::max(scr_in, fused_heads_bytes(npos, d.role_count, lgrow, gap_features(d), c.nb,
-                                                                           c.threads == 512 ? 1 : c.nb))
+                                                                           c.groups == 2 ? 1 : c.nb, fpad))
                                       : scr_in;
         t.btab_off = c.single_image ? align16(std::max(c.act_bytes, scr))
                                     : c.nb * c.act_bytes + std::max(c.nb * c.act_bytes, scr);

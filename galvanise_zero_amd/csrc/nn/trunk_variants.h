@@ -22,7 +22,8 @@ struct KernelChoice {
     int nb = 1;
     bool single_image = false;
     int resid_bytes = 0;           // global residual scratch per workgroup (0: registers)
-    int threads = 256;             // workgroup size (512: two wave groups, trunk_kernel8)
+    int threads = 256;             // workgroup size (512: trunk_kernel8 / trunk_kernel_w8)
+    int groups = 1;                // wave groups (2: trunk_kernel8, a board per group)
     char name[64] = {0};           // the kernel as rocprofv3 names it
 };
 
@@ -47,7 +48,20 @@ KernelChoice kernel8_for() {
     k.act_bytes = Geo<F, PTN, 1, P, 2>::ACT_BYTES;
     k.nb = 2;
     k.threads = 512;
+    k.groups = 2;
     std::snprintf(k.name, sizeof(k.name), "gznn::trunk_kernel8<%d, %d, %d>", F, PTN, P);
+    return k;
+}
+
+// one group of 8 waves for two boards (variant 24)
+template <int F, int PTN, int P>
+KernelChoice kernelw8_for() {
+    KernelChoice k;
+    k.fn = (const void*)&trunk_kernel_w8<F, PTN, P>;
+    k.act_bytes = Geo<F, PTN, 2, P, 3>::ACT_BYTES;
+    k.nb = 2;
+    k.threads = 512;
+    std::snprintf(k.name, sizeof(k.name), "gznn::trunk_kernel_w8<%d, %d, %d>", F, PTN, P);
     return k;
 }
 
@@ -74,8 +88,11 @@ KernelChoice variants(int v, int precision) {
                 // two boards per workgroup (F = 128: 256-byte wrapped rows, hi + lo in 512 bytes)
                 if constexpr (Geo<F, PTN, 1, 3>::WRAP && 4 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024) {
                     if (v == 21) return kernel_for<F, PTN, 2, 1, 3, V2>();
-                    if constexpr (!V2)
+                    if constexpr (!V2) {
                         if (v == 22) return kernel8_for<F, PTN, 3>();
+                        if constexpr (F == 128)
+                            if (v == 24) return kernelw8_for<F, PTN, 3>();
+                    }
                 }
             }
         }

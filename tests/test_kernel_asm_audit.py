@@ -61,7 +61,7 @@ def test_auditor_rule3_loop_copy():
 
 
 # every trunk instantiation that runs the split looped conv (the F = 128 split kernels, v1 and v2,
-# one and two boards, the two-group kernel), in one translation unit
+# one and two boards, the two-group and the 8-wave kernels), in one translation unit
 AUDIT_TU = """#include "trunk_variants.h"
 namespace gznn {
 template __global__ void trunk_kernel<128, 2, 1, 1, 3>(KParams);
@@ -73,6 +73,9 @@ template __global__ void trunk_kernel<128, 4, 2, 1, 3>(KParams);
 template __global__ void trunk_kernel_v2<128, 4, 1, 1, 3>(KParams);
 template __global__ void trunk_kernel_v2<128, 4, 2, 1, 3>(KParams);
 template __global__ void trunk_kernel8<128, 4, 3>(KParams);
+template __global__ void trunk_kernel_w8<128, 2, 3>(KParams);
+template __global__ void trunk_kernel_w8<128, 3, 3>(KParams);
+template __global__ void trunk_kernel_w8<128, 4, 3>(KParams);
 }
 """
 
@@ -86,7 +89,7 @@ def test_compiled_chains_hazard_free(tmp_path):
                            "--cuda-device-only", "-S", "-I", NN, "-o", str(out), str(src)],
                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     res = kaa.audit(out.read_text())
-    assert len(res) == 9, sorted(res)     # every instantiation above runs chains
+    assert len(res) == 12, sorted(res)    # every instantiation above runs chains
     for name, (n, bad) in res.items():
         assert n > 0
         assert bad == [], (name, bad[:5])
