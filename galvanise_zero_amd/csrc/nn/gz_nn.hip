@@ -92,9 +92,12 @@ extern "C" const char* gz_nn_last_error(void) { return g_err.c_str(); }
 // choosing per launch keeps results batch-invariant.
 // Launches of 257-383 rows also take the two-board kernel: at one board per workgroup they would
 // need a second wave of workgroups on the 256 CUs (one trunk workgroup per CU by LDS).
-// large launches: the 8-wave two-board kernel where compiled (F = 128 split v1 nets: 5 % faster than
-// 21 at the runner's 1,024-row launches, bit-identical; profiles/r04t_w8_kexp.txt), else 21
-constexpr int kSmallVariant = 11, kLargeVariant = 24, kLargeFallback = 21, kLargeMinRows = 257;
+// large launches: the two-board 4-wave kernel (21).  The 8-wave kernel (24) is 5 % faster back to
+// back (profiles/r04t_w8_kexp.txt) but equal inside the bench, whose launches arrive with gaps
+// (0.4954 vs 0.4942 ms per 1,024-row launch, same box; profiles/r04x_variants_in_bench.txt):
+// selectable (GZ_KERNEL_VARIANT=24), bit-identical.  kLargeFallback: where kLargeVariant is not
+// compiled for a geometry.
+constexpr int kSmallVariant = 11, kLargeVariant = 21, kLargeFallback = 21, kLargeMinRows = 257;
 constexpr int kCUs = 256;
 
 static KernelChoice select_kernel(int fpad, int pt, int v, int precision, bool v2) {
