@@ -145,6 +145,11 @@ constexpr bool kLoopSI = false;
 // scratch and its hi parts into the image, in one pass (instead of lo parts into the image, a
 // copy-out sweep, then the hi parts)
 constexpr bool kLoDirect = true;
+// Two-image v1 kernels: each conv's epilogue inside its last k-step (conv3x3_looped EPI).  Measured
+// no faster (bit-identical; residual trunk 490.7 k vs 489.4 k cycles per workgroup,
+// profiles/r04z_epilogue_in_conv_kexp.txt): with one wave per SIMD the epilogue's VALU work issues in
+// order between the MFMA chains and outlasts their shadow, so off; kept for experiments (kexp epioff)
+constexpr bool kEpiInConv = false;
 
 // ring depth: largest R dividing the stages per conv with R slots of KS*CT fragments <= cap VGPRs
 __host__ __device__ constexpr int ring_depth(int nst, int ks, int ct, int cap) {
@@ -625,12 +630,29 @@ __device__ __forceinline__ void split_chain_leave(f32x4 (&acc)[CT][TT]) {
         for (int t = 0; t < TT; ++t) asm volatile("" : "+a"(acc[ct][t]));
 }
 
-template <int F, int PTN, int NB, int P, int WG, int PASS, int ST>
+// No epilogue inside the conv (the default)
+struct NoEpi {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+
+// EPI (the conv's last iteration): the epilogue of position tile t - 1 runs right after tile t's MFMAs
+// of the conv's final k-step (and tile TT - 1's after the last), so the epilogue's VALU work overlaps
+// the remaining MFMAs instead of following them all.  Its reads of tile t - 1's accumulators come
+// behind a 20-state pad pinned to them (MFMA D -> VALU read; split kernels' asm chains).  The
+// epilogue writes the OTHER image (two-image kernels), which no wave reads in this conv.
+template <int CT, int TT>
+__device__ __forceinline__ void tile_leave(f32x4 (&acc)[CT][TT], int t) {
+    asm volatile("s_nop 15\n\ts_nop 3" ::: "memory");
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) asm volatile("" : "+a"(acc[ct][t]));
+}
+
+template <int F, int PTN, int NB, int P, int WG, int PASS, int ST, bool EPI = false, class Epi = NoEpi>
 __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                              f32x4 (&acc)[Geo<F, PTN, NB, P, WG>::CT][Geo<F, PTN, NB, P, WG>::TT],
                                              bf16x8 (&b)[Geo<F, PTN, NB, P, WG>::TT][Geo<F, PTN, NB, P, WG>::P2],
                                              const __bf16* wres, uint32_t woff, int gs_it, int gmax, int& lane,
-                                             const Board& bd, int tap0, bool last_it) {
+                                             const Board& bd, int tap0, bool last_it, const Epi& epi = Epi{}) {
     using G = Geo<F, PTN, NB, P, WG>;
     constexpr int R = G::R, KS = G::KS, CT = G::CT, PT = G::PT, KC = G::KC, P2 = G::P2, WP = G::WP;
     static_assert(P != 2 || G::TRACKED, "two-pass split: compiler-tracked weight loads");
@@ -690,26 +712,41 @@ __device__ __forceinline__ void conv_stage_l(const char* __restrict__ X, Ring<F,
                     __builtin_amdgcn_sched_group_barrier(0x008, CT * (P == 2 && PASS == 0 ? 2 : 1), 0);   // MFMA
                     __builtin_amdgcn_sched_group_barrier(0x100, P2, 0);                                 // DS read
                 }
+                if constexpr (EPI && ST == G::U - 1) {
+                    if (k == KS - 1 && t >= 1) {
+                        if constexpr (P2 == 2) tile_leave(acc, t - 1);
+                        epi(t - 1);
+                    }
+                }
             }
+        if constexpr (EPI && ST == G::U - 1) {
+            if (k == KS - 1) {
+                if constexpr (P2 == 2) tile_leave(acc, G::TT - 1);
+                epi(G::TT - 1);
+            }
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-template <int F, int PTN, int NB, int P, int WG, int PASS, int... ST>
+template <int F, int PTN, int NB, int P, int WG, int PASS, bool EPI, class Epi, int... ST>
 __device__ __forceinline__ void conv_iter(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                           f32x4 (&acc)[Geo<F, PTN, NB, P, WG>::CT][Geo<F, PTN, NB, P, WG>::TT],
                                           bf16x8 (&b)[Geo<F, PTN, NB, P, WG>::TT][Geo<F, PTN, NB, P, WG>::P2],
                                           const __bf16* wres, uint32_t woff, int gs_it, int gmax, int& lane,
-                                          const Board& bd, int tap0, bool last_it, std::integer_sequence<int, ST...>) {
-    (conv_stage_l<F, PTN, NB, P, WG, PASS, ST>(X, ring, acc, b, wres, woff, gs_it, gmax, lane, bd, tap0, last_it), ...);
+                                          const Board& bd, int tap0, bool last_it, const Epi& epi,
+                                          std::integer_sequence<int, ST...>) {
+    (conv_stage_l<F, PTN, NB, P, WG, PASS, ST, EPI, Epi>(X, ring, acc, b, wres, woff, gs_it, gmax, lane, bd, tap0, last_it,
+                                                         epi), ...);
 }
 
-// PASS (P = 2): 0 starts the accumulators, 1 adds to them
-template <int F, int PTN, int NB, int P, int WG = 1, int PASS = 0>
+// PASS (P = 2): 0 starts the accumulators, 1 adds to them.  EPI: the epilogue epi(t) of every
+// position tile runs inside the last iteration (conv_stage_l), the last iteration peeled.
+template <int F, int PTN, int NB, int P, int WG = 1, int PASS = 0, bool EPI = false, class Epi = NoEpi>
 __device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<F, PTN, NB, P, WG>& ring,
                                                f32x4 (&acc)[Geo<F, PTN, NB, P, WG>::CT][Geo<F, PTN, NB, P, WG>::TT],
                                                const __bf16* wres, uint32_t woff, int gs0, int gmax, int lane,
-                                               const Board& bd) {
+                                               const Board& bd, const Epi& epi = Epi{}) {
     using G = Geo<F, PTN, NB, P, WG>;
     constexpr int PT = G::PT, TT = G::TT;
     if constexpr (PASS == 0) {
@@ -729,10 +766,15 @@ __device__ __forceinline__ void conv3x3_looped(const char* __restrict__ X, Ring<
             for (int h = 0; h < G::P2; ++h) b[bb * PT + pt][h] = *(const bf16x8*)(a + bb * G::ACT_BYTES + h * G::HALF);
     }
     if constexpr (G::P2 == 2) split_chain_enter(acc);
+    constexpr int NLOOP = EPI ? G::NIT - 1 : G::NIT;
 #pragma clang loop unroll(disable)
-    for (int it = 0; it < G::NIT; ++it)
-        conv_iter<F, PTN, NB, P, WG, PASS>(X, ring, acc, b, wres, woff, gs0 + it * G::U, gmax, lane, bd, it * G::TPI,
-                                       it == G::NIT - 1, std::make_integer_sequence<int, G::U>{});
+    for (int it = 0; it < NLOOP; ++it)
+        conv_iter<F, PTN, NB, P, WG, PASS, false, NoEpi>(X, ring, acc, b, wres, woff, gs0 + it * G::U, gmax, lane, bd,
+                                                       it * G::TPI, it == G::NIT - 1, NoEpi{},
+                                                       std::make_integer_sequence<int, G::U>{});
+    if constexpr (EPI)
+        conv_iter<F, PTN, NB, P, WG, PASS, true, Epi>(X, ring, acc, b, wres, woff, gs0 + NLOOP * G::U, gmax, lane, bd,
+                                                   NLOOP * G::TPI, true, epi, std::make_integer_sequence<int, G::U>{});
     if constexpr (G::P2 == 2) split_chain_leave(acc);
 }
 
@@ -1248,6 +1290,45 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
         const float* b_a = btab + (2 * blk) * F;
         const float* b_b = b_a + F;
 
+        if constexpr (!V2 && G::LOOP && kEpiInConv) {
+            // the same two epilogues as below, run per position tile inside each conv's last k-step
+            float4 bia[CT];
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) bia[ct] = *(const float4*)(b_a + co_base + 16 * ct + 4 * g);
+            auto epi1 = [&](int t) {
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) {
+                    f32x4 v = acc[ct][t];
+                    v[0] = act_mx(v[0] + bia[ct].x, alpha);
+                    v[1] = act_mx(v[1] + bia[ct].y, alpha);
+                    v[2] = act_mx(v[2] + bia[ct].z, alpha);
+                    v[3] = act_mx(v[3] + bia[ct].w, alpha);
+                    store_act<F, PTN, P, !G::SI>(X1 + (t / PT) * ACT, 16 * (t % PT) + li, co_base + 16 * ct + 4 * g, v, NPOS);
+                }
+            };
+            conv3x3_looped<F, PTN, NB, P, WG, 0, true>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd, epi1);
+            __syncthreads();
+            float4 bib[CT];
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) bib[ct] = *(const float4*)(b_b + co_base + 16 * ct + 4 * g);
+            auto epi2 = [&](int t) {
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) {
+                    f32x4 v = acc[ct][t];
+                    const f32x4 r = resid[ct][t];
+                    v[0] = act_mx(v[0] + bib[ct].x + r[0], alpha);
+                    v[1] = act_mx(v[1] + bib[ct].y + r[1], alpha);
+                    v[2] = act_mx(v[2] + bib[ct].z + r[2], alpha);
+                    v[3] = act_mx(v[3] + bib[ct].w + r[3], alpha);
+                    resid[ct][t] = v;
+                    acc[ct][t] = v;
+                    store_act<F, PTN, P, !G::SI>(X0 + (t / PT) * ACT, 16 * (t % PT) + li, co_base + 16 * ct + 4 * g, v, NPOS);
+                }
+            };
+            conv3x3_looped<F, PTN, NB, P, WG, 0, true>(X1, ring, acc, kp.wres, woff, (2 * blk + 1) * G::NST, gmax, lane, bd, epi2);
+            __syncthreads();
+            continue;
+        }
         if constexpr (G::LOOP) conv3x3_looped<F, PTN, NB, P, WG>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd);
         else conv3x3<F, PTN, NB, P, WG>(X0, ring, acc, kp.wres, woff, (2 * blk) * G::NST, gmax, lane, bd);
 #pragma unroll

@@ -16,6 +16,7 @@ libgz_engine.so.  Timing on the GPU box: GZ_LIB_DIR=tools/kexp/lib_<name> python
   ring6/ring12 the two-board split kernel's weight ring 6 / 12 stages deep instead of one tap (4)
   lounroll16   the two-pass kernel's lo-image copies 16 uint4 per thread in flight instead of 4
   nolocopy     the two-pass kernel skips the lo-image copies (results wrong; their cost)
+  epion        the two-image kernels' epilogues inside the conv's last k-step instead of after it
   lodirectoff  the two-pass kernel's epilogues write the lo parts into the image and sweep them out
                (round-3 / r04n scheme) instead of straight to the scratch
   a+b          both patches
@@ -79,6 +80,8 @@ def patch(name, text):  # noqa: C901
         rep("#pragma unroll 4\n    for (int i = tid; i < n16; i += 256) {", "#pragma unroll 16\n    for (int i = tid; i < n16; i += 256) {")
     elif name == "nolocopy":
         rep("    for (int i = tid; i < n16; i += 256) {", "    for (int i = tid; i < n16 && npos < 0; i += 256) {")
+    elif name == "epion":
+        rep("constexpr bool kEpiInConv = false;", "constexpr bool kEpiInConv = true;")
     elif name == "lodirectoff":
         rep("constexpr bool kLoDirect = true;", "constexpr bool kLoDirect = false;")
     elif name == "noheads":
