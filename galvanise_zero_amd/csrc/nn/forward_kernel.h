@@ -151,6 +151,13 @@ constexpr bool kLoDirect = true;
 // order between the MFMA chains and outlasts their shadow, so off; kept for experiments (kexp epioff)
 constexpr bool kEpiInConv = false;
 
+// Split two-image kernels' epilogue stores (store_act): one 16-byte store per lane after a lane swap
+// instead of two 8-byte stores (whose 16 positions per store at the 544-byte row stride share banks
+// two ways).  Bit-identical but no faster (profiles/r04za_store_swap_kexp.txt: 0.543-0.547 against
+// 0.547-0.549 ms per 1,024-row launch, residual blocks 79.3 against 78.4 us): the stores are off the
+// critical path, so off; kept for experiments (kexp swapon)
+constexpr bool kStoreSwap = false;
+
 // ring depth: largest R dividing the stages per conv with R slots of KS*CT fragments <= cap VGPRs
 __host__ __device__ constexpr int ring_depth(int nst, int ks, int ct, int cap) {
     const int cand[5] = {9, 6, 4, 3, 2};
@@ -308,6 +315,21 @@ __device__ __forceinline__ float bf16_lo(float x) { return x - (float)(__bf16)x;
 template <int F, int PTN, int P = 1, bool SEL = true>
 __device__ __forceinline__ void store_act(char* X, int p, int co, f32x4 v, int npos) {
     using G = Geo<F, PTN, 1, P>;
+    if constexpr (SEL && G::WRAP && kStoreSwap) {
+        // Split two-image kernels: the lanes of rows 2r and 2r + 1 (channel groups g, g + 1 of one
+        // position) trade halves with one v_permlane16_swap per dword, so row 2r holds the hi parts of
+        // the 8 channels and row 2r + 1 their lo parts: one 16-byte store per lane (the chunk's hi
+        // half, or its lo half at + HALF) instead of two 8-byte stores, the same bytes in the image.
+        // (Every lane takes part: no branch around it.)
+        const int q = p >= npos ? npos + G::ZROWS : p;
+        const uint32_t h0 = pack2(v[0], v[1]), h1 = pack2(v[2], v[3]);
+        const uint32_t l0 = pack2(bf16_lo(v[0]), bf16_lo(v[1])), l1 = pack2(bf16_lo(v[2]), bf16_lo(v[3]));
+        const auto s0 = __builtin_amdgcn_permlane16_swap(h0, l0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(h1, l1, false, false);
+        char* a = X + q * G::ROWS + ((co >> 3) << 4) + ((co & 4) ? G::HALF : 0);
+        *(uint4*)a = uint4{s0[0], s1[0], s0[1], s1[1]};
+        return;
+    }
     if (SEL || p < npos) {
         const int q = SEL && p >= npos ? npos + G::ZROWS : p;
         const int chunk = G::WRAP ? (co >> 3) : ((co >> 3) + swz(q));

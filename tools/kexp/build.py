@@ -19,6 +19,8 @@ libgz_engine.so.  Timing on the GPU box: GZ_LIB_DIR=tools/kexp/lib_<name> python
   epion        the two-image kernels' epilogues inside the conv's last k-step instead of after it
   lodirectoff  the two-pass kernel's epilogues write the lo parts into the image and sweep them out
                (round-3 / r04n scheme) instead of straight to the scratch
+  swapon       the split two-image epilogues store one 16-byte chunk half per lane after a lane swap
+               instead of two 8-byte halves (kStoreSwap)
   a+b          both patches
   full_<name>  patch <name>, build every trunk instantiation (the deep configs' F = 256 kernels)
 Usage: python tools/kexp/build.py base nostore ...
@@ -84,6 +86,8 @@ def patch(name, text):  # noqa: C901
         rep("constexpr bool kEpiInConv = false;", "constexpr bool kEpiInConv = true;")
     elif name == "lodirectoff":
         rep("constexpr bool kLoDirect = true;", "constexpr bool kLoDirect = false;")
+    elif name == "swapon":
+        rep("constexpr bool kStoreSwap = false;", "constexpr bool kStoreSwap = true;")
     elif name == "noheads":
         rep("        dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);", "        if (nb < 0) dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);")
     elif name == "siunroll":
