@@ -13,6 +13,7 @@ libgz_engine.so.  Timing on the GPU box: GZ_LIB_DIR=tools/kexp/lib_<name> python
   siunroll     the single-image kernels' fully unrolled conv (round 3) instead of the looped one
   headsunroll  the dense heads' weight loops unrolled 128 (policy) / 64 (value) instead of 32
   noheads      the fused trunk kernels skip the dense heads (results wrong; their cost)
+  nophaseb     the two-phase dense heads skip phase B (softmax / value waves; results wrong)
   ring6/ring12 the two-board split kernel's weight ring 6 / 12 stages deep instead of one tap (4)
   lounroll16   the two-pass kernel's lo-image copies 16 uint4 per thread in flight instead of 4
   nolocopy     the two-pass kernel skips the lo-image copies (results wrong; their cost)
@@ -89,7 +90,9 @@ def patch(name, text):  # noqa: C901
     elif name == "swapon":
         rep("constexpr bool kStoreSwap = false;", "constexpr bool kStoreSwap = true;")
     elif name == "noheads":
-        rep("        dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);", "        if (nb < 0) dense_heads<NBW, kThreads * WG>(kp, fk, lg, wb0, nb);")
+        rep("        dense_heads<NBW, kThreads * NGR>(kp, fk, lg, wb0, nb);", "        if (nb < 0) dense_heads<NBW, kThreads * NGR>(kp, fk, lg, wb0, nb);")
+    elif name == "nophaseb":
+        rep("    const int ntask = R * nb + nb;\n", "    const int ntask = nb < 0 ? R * nb + nb : 0;\n")
     elif name == "siunroll":
         rep("    static constexpr bool LOOPSI = SI && NST % US == 0 && NST / US >= 2;\n",
             "    static constexpr bool LOOPSI = false;\n")
