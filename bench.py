@@ -324,7 +324,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from galvanise_zero_amd._native import HipNet
+    from galvanise_zero_amd._native import HipNet, engine_build_info
     from galvanise_zero_amd.nn.weights import random_weights, to_blob
     from galvanise_zero_amd.runner import SelfPlayRunner
     from galvanise_zero_amd import shard
@@ -406,7 +406,11 @@ def main():
             blob2.copy_(torch.from_numpy(to_blob(random_weights(desc, 7922))))
         shard.broadcast_weights(blob2, src=0)
         torch.cuda.synchronize()
+        tr = time.perf_counter()
         roll = runner.update_network(device_ptr=blob2.data_ptr(), count=net.weight_count, clear_unique_states=True)
+        # the caller's wait: handed to the launcher, applied between two launches (BN fold + bf16 pack
+        # on the device, gz_net_set_weights_device), filters cleared
+        roll["ms"] = (time.perf_counter() - tr) * 1e3
         roll_sum = float(blob2.double().sum().item())
     # ---- warmup + timed steps --------------------------------------------------------------------
     rows_base = aged["rows"]
@@ -554,7 +558,8 @@ def main():
                          "flop_per_leaf": flops, "aggregate_tflops": flops * rows / T / 1e12},
             "gpu_busy_frac": (kms / 1e3) / (T * world) if T > 0 else None,
             "split_launches": split_launches,
-            "generation_roll": {"launches_before_rank0": roll["launches_before"],
+            "generation_roll": {"launches_before_rank0": roll["launches_before"], "ms_rank0": roll["ms"],
+                                "apply_ms_rank0": roll.get("apply_ms"),
                                 "collective": "RCCL broadcast" if world > 1 and args.backend == "nccl" else args.backend,
                                 "identical_on_all_ranks": abs(roll_sums - world * roll_sum) <= 1e-6 * max(1.0, abs(world * roll_sum))}
                                if roll else None,
@@ -568,6 +573,7 @@ def main():
                        if opening else None,
             "engine_idle_frac": (idle_ms / 1e3) / (T * world * threads) if T > 0 else None,
             "host_peak_rss_gb": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6,
+            "engine_build": engine_build_info(),
         }
         if dom:
             out["roofline"]["l2_weight_stream"] = per_variant[dom]["l2_weight_stream"]

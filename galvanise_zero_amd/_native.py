@@ -89,6 +89,10 @@ def nn_lib():
         lib.gz_net_weight_count.argtypes = [ctypes.c_void_p]
         lib.gz_net_set_weights.argtypes = [ctypes.c_void_p, _FP, ctypes.c_size_t]
         lib.gz_net_set_weights_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        lib.gz_net_last_roll_ms.restype = ctypes.c_double
+        lib.gz_net_last_roll_ms.argtypes = [ctypes.c_void_p]
+        lib.gz_net_copy_weight_image.restype = ctypes.c_size_t
+        lib.gz_net_copy_weight_image.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         lib.gz_net_forward.argtypes = [ctypes.c_void_p, _FP, ctypes.c_int,
                                        ctypes.POINTER(_FP), _FP]
         lib.gz_net_forward_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -173,6 +177,19 @@ class HipNet(object):
     def set_weights_device(self, ptr, count):
         self._check(self.lib.gz_net_set_weights_device(self.handle, ctypes.c_void_p(ptr), count),
                     "gz_net_set_weights_device")
+
+    def last_roll_ms(self):
+        """Device milliseconds of the last set_weights_device (BN fold + bf16 pack kernels)."""
+        return self.lib.gz_net_last_roll_ms(self.handle)
+
+    def weight_image(self):
+        """The packed device weight image as bytes (diagnostics: host and device packing compare)."""
+        n = self.lib.gz_net_copy_weight_image(self.handle, None, 0)
+        buf = np.empty(n, dtype=np.uint8)
+        got = self.lib.gz_net_copy_weight_image(self.handle, buf.ctypes.data, n)
+        if got != n:
+            raise RuntimeError("gz_net_copy_weight_image failed")
+        return buf
 
     def forward(self, planes):
         d = self.desc
@@ -399,6 +416,7 @@ _ENGINE_SIGS = {
     "gz_pool_add_ordinal_stats": (ctypes.c_int, [_VP, _VP]),
     "gz_engine_set_verify_fastpath": (ctypes.c_int, [ctypes.c_int]),
     "gz_engine_verified_decisions": (ctypes.c_long, []),
+    "gz_engine_build_info": (ctypes.c_char_p, []),
 }
 
 
@@ -509,8 +527,15 @@ def runner_lib():
         lib.gz_runner_last_error.restype = ctypes.c_char_p
         lib.gz_runner_clear_unique_states.argtypes = [_VP]
         lib.gz_runner_update_network.argtypes = [_VP, _VP, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_double]
+        lib.gz_runner_roll_apply_ms.restype = ctypes.c_double
+        lib.gz_runner_roll_apply_ms.argtypes = [_VP]
         lib.gz_runner_roll_info.argtypes = [_VP, ctypes.POINTER(ctypes.c_long), ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_long)]
         lib.gz_runner_ordinal_stats.argtypes = [_VP, ctypes.POINTER(GzOrdinalStats)]
         lib._gz_runner_typed = True
     return lib
+
+
+def engine_build_info():
+    """How libgz_engine.so was built: "pgo=<use|none|stale|gen> march=<...>" (csrc/Makefile)."""
+    return engine_lib().gz_engine_build_info().decode()

@@ -540,6 +540,13 @@ extern "C" int gz_engine_set_verify_fastpath(int on) {
     return prev ? 1 : 0;
 }
 extern "C" long gz_engine_verified_decisions(void) { return verified_decisions(); }
+#ifndef GZ_BUILD_PGO
+#define GZ_BUILD_PGO "unknown"
+#endif
+#ifndef GZ_BUILD_MARCH
+#define GZ_BUILD_MARCH "unknown"
+#endif
+extern "C" const char* gz_engine_build_info(void) { return "pgo=" GZ_BUILD_PGO " march=" GZ_BUILD_MARCH; }
 extern "C" long gz_pool_take_sample_count(gz_pool* p) {
     std::vector<Sample*>& s = p->impl->getSamples();
     const long n = (long)s.size();

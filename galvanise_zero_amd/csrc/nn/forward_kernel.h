@@ -127,7 +127,7 @@ __device__ __forceinline__ void dense_heads(const KParams& kp, const float* fk, 
 
 // The board geometry at run time (kernels are compiled per filter count and position-tile count):
 // p / W as (p * ceil(65536 / W)) >> 16, exact for W <= 32 and p < 1024 (checked on the host).
-constexpr int kMaxPTN = 11;        // position tiles of the largest compiled board (13 x 13)
+constexpr int kMaxPTN = 23;        // position tiles of the largest compiled board (19 x 19)
 struct Board {
     int H, W, npos, wmagic;
     // per lane and position tile pt (position p = 16 pt + lane % 16): bit tap (0-8) says whether p
@@ -206,7 +206,11 @@ struct Geo {
     // whose 16-byte bank group (34 q + c) mod 16 = (2 q + c) mod 16 is the rotated layout's --
     // so a k-step's B reads differ by immediate offsets again (no add + and per read).  Off-board
     // neighbours read a zero area (two rows) at the rotated chunk of their virtual position.
-    static constexpr bool WRAP = CPR >= 16 && P2 == 2;
+    // Large boards (more than 11 position tiles, up to 19 x 19: one part per row, two-pass split)
+    // take the same padded rows for their single part: ROWS = 16 CPR + 32, bank group
+    // (18 q + c) mod 16 = (2 q + c) mod 16 again (F = 128: 288 bytes a row, the 19 x 19 image 107 KB,
+    // where the rotated 512-byte rows would need 190 KB)
+    static constexpr bool WRAP = CPR >= 16 && (P2 == 2 || PTN > 11);
     static constexpr int HALF = WRAP ? CPR * 16 : ((CPR + 14) * 16 + 255) & ~255;   // one part's row
     static constexpr int ROWS = WRAP ? P2 * HALF + 32 : P2 * HALF;   // LDS row stride: hi part, then lo part
     static constexpr int ZROWS = WRAP ? 2 : 1;       // zero rows (padded rows: reads up to ROWS + 512)
@@ -235,13 +239,16 @@ struct Geo {
     // live VGPRs of the trunk loop: weight ring + double-buffered B fragments + accumulators +
     // residual stream
     static constexpr int LIVE_VGPRS = R0 * KS * NFR * 4 + 2 * TT * P2 * 4 + 2 * CT * TT * 4;
-    static constexpr bool SI = 2 * NB * ACT_BYTES + 16 * 1024 > 160 * 1024 || (NB == 1 && LIVE_VGPRS > 330);
+    // (the two-pass split kernels, P = 2, are single-image by construction)
+    static constexpr bool SI = 2 * NB * ACT_BYTES + 16 * 1024 > 160 * 1024 || (NB == 1 && LIVE_VGPRS > 330) || P == 2;
     // ring depth: single-image kernels run the looped conv (single-buffered B fragments), which
     // leaves room for a deeper ring (up to 128 VGPRs: F = 256 split, 4 stages = 3 k-steps ahead of
     // the MFMAs; its weights stream from the MALL, not the L2)
     static constexpr int RS = ring_depth(NST, KS, NFR, 64);
     static constexpr int US = lcm_c(RS, KC / KS) * ((lcm_c(RS, KC / KS) * KS) % 2 ? 2 : 1);
-    static constexpr bool LOOPSI = kLoopSI && SI && NST % US == 0 && NST / US >= 2;
+    // (large boards always loop: the unrolled conv's double-buffered B fragments alone would take
+    // 2 x 23 x 4 VGPRs beside 184 accumulators)
+    static constexpr bool LOOPSI = (kLoopSI || PTN > 11) && SI && NST % US == 0 && NST / US >= 2;
     static constexpr int R = LOOPSI ? RS : R0;
     static constexpr int LPS = KS * NFR;             // weight loads per stage per lane
     // Global residual: when the fp32 residual stream (+ the accumulators) would need more than 256
@@ -358,7 +365,7 @@ template <int F, int PTN>
 __device__ __forceinline__ void store_lo_scratch(char* xlo, int p, int co, f32x4 v, int npos) {
     using G = Geo<F, PTN, 1, 2>;
     if (p < npos) {
-        const int chunk = (co >> 3) + swz(p);
+        const int chunk = G::WRAP ? (co >> 3) : (co >> 3) + swz(p);
         uint2 l;
         l.x = pack2(bf16_lo(v[0]), bf16_lo(v[1]));
         l.y = pack2(bf16_lo(v[2]), bf16_lo(v[3]));
@@ -931,7 +938,7 @@ __device__ __forceinline__ void save_lo_write_hi(char* X, char* xlo, const f32x4
 template <int F, int PTN, int NB, int WPE, int P, bool V2, int WG = 1>
 __device__ __forceinline__ void trunk_body(const KParams& kp) {
     using G = Geo<F, PTN, NB, P, WG>;
-    static_assert(P == 1 || (P == 3 && (NB == 1 || G::WRAP) && (G::CT <= 2 || G::SI)) || (P == 2 && G::SI && !V2),
+    static_assert(P == 1 || (P == 3 && (NB == 1 || G::WRAP) && (G::CT <= 2 || G::SI)) || (P == 2 && G::SI && (!V2 || kLoDirect)),
                   "split precision: F <= 128 (F = 256: single image)");
     constexpr int P2 = G::P2;
     constexpr int IP2 = G::WP;    // bf16 parts of the initial conv's operands (im2col scratch, w0 / w0lo)
@@ -1018,6 +1025,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     // device feature scratch, which heads_kernel reads.  The partials are rewritten only after at
     // least one more barrier (the next block's first epilogue), so one buffer serves every layer.
     float* calp = (float*)(smem + kp.cal_off);   // [4 waves][NB][NPOS]
+    // (gz_nn.hip sizes cal_off's buffer and cal_reduce sums for exactly four waves)
+    static_assert(!V2 || NWV == 4, "concat_all_layers partials: four waves per group");
     auto cal_partial = [&](int j, int bb) {
         float4 wv[CT];
 #pragma unroll
@@ -1062,7 +1071,13 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     char* IM = SCR + align16(C * NPOS * 4);
     const int imrow = K0 * 2;
     char* IMlo = IM + align16((NPOS + 1) * imrow);   // split precision: lo parts of the inputs
-    const int imswz = ((K0 >> 3) < 16 ? (K0 >> 3) : 16) - 1;
+    // chunk swizzle of an im2col row: XOR with (p & imswz) must map the row's K0 / 8 chunks onto
+    // themselves, so imswz + 1 is the largest power of two (<= 16) dividing the chunk count (K0 = 32,
+    // 64, 128: 3, 7, 15).  (Rounds 1-4 took min(chunks, 16) - 1, which for K0 = 96 / 160 / 224 -- a
+    // 3x3 initial conv over 8-10 / 15-17 / 22-24 planes -- sent chunks past the row into the next
+    // position's: the draughts model file f1_581 computed wrong inputs, hidden in bf16's tolerance.)
+    const int nch0 = K0 >> 3;
+    const int imswz = ((nch0 & -nch0) < 16 ? (nch0 & -nch0) : 16) - 1;
     // initial-conv weights one k-step ahead of their MFMAs (each step's fragments would otherwise
     // wait a full L2 round trip); the first step's are the same for every board: issued here, with
     // the input planes still in flight
@@ -1180,8 +1195,9 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                 else resid[ct][bb * PT + pt] = v;
                 acc[ct][bb * PT + pt] = v;    // the heads read acc when there is no residual block
                 if constexpr (P == 2 && kLoDirect) {
-                    store_act<F, PTN, 1, false>(X0 + bb * ACT, 16 * pt + li, co, v, NPOS);
-                    store_lo_scratch<F, PTN>(xlo, 16 * pt + li, co, v, NPOS);
+                    const f32x4 sv = preact ? pre_act(v, psc, psh, kp.leaky) : v;
+                    store_act<F, PTN, 1, false>(X0 + bb * ACT, 16 * pt + li, co, sv, NPOS);
+                    store_lo_scratch<F, PTN>(xlo, 16 * pt + li, co, sv, NPOS);
                 } else {
                     store_act<F, PTN, P, !G::SI>(X0 + bb * ACT, 16 * pt + li, co, preact ? pre_act(v, psc, psh, kp.leaky) : v, NPOS);
                 }
@@ -1261,7 +1277,15 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
                         if constexpr (RG) rgc[(ct * TT + t) * 64] = v;
                         else resid[ct][t] = v;
                         acc[ct][t] = v;
-                        if (more) store_act<F, PTN, P, !G::SI>(X0, 16 * t + li, co, pre_act(v, psc, psh, kp.leaky), NPOS);
+                        if (more) {
+                            const f32x4 pv = pre_act(v, psc, psh, kp.leaky);
+                            if constexpr (P == 2) {   // (two-pass split: hi parts to the image, lo to the scratch)
+                                store_act<F, PTN, 1, false>(Xe, 16 * t + lie, co, pv, NPOS);
+                                store_lo_scratch<F, PTN>(xloe, 16 * t + lie, co, pv, NPOS);
+                            } else {
+                                store_act<F, PTN, P, !G::SI>(X0, 16 * t + li, co, pv, NPOS);
+                            }
+                        }
                     }
                 }
                 if (kp.cal)   // layer blk + 1: the block's add

@@ -56,6 +56,8 @@ struct gz_net {
     int p2 = 1;                    // bf16 parts per operand: 1 (bf16) or 2 (split precision)
     int fpad = 0;                  // filters rounded up to the compiled 64 / 128 / 256 (zero channels)
     bool has_weights = false;
+    size_t image_bytes = 0;        // bytes of the device weight image
+    float last_roll_ms = 0.f;      // device time of the last gz_net_set_weights_device
 
     char* dmem = nullptr;          // all weights, one allocation
     KParams kp{};                  // weight pointers filled in, outputs per launch
@@ -106,9 +108,8 @@ static KernelChoice select_kernel(int fpad, int pt, int v, int precision, bool v
 }
 
 // ---- bf16 (round to nearest even) -------------------------------------------------------------
-static inline uint16_t f2bf(float f) {
-    uint32_t u;
-    std::memcpy(&u, &f, 4);
+static inline __host__ __device__ uint16_t f2bf(float f) {
+    uint32_t u = __builtin_bit_cast(uint32_t, f);
     if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
     u += 0x7fffu + ((u >> 16) & 1u);
     return (uint16_t)(u >> 16);
@@ -167,9 +168,9 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
     }
     // kernels are compiled per padded filter count and position-tile count; the board's H and W
     // are kernel arguments (H = input_columns, W = input_rows: bases.py:104-121)
-    const int fpad = padded_filters(d.cnn_filter_size);
     const int npos_ = d.input_columns * d.input_rows;
-    const int pt = (npos_ + 15) / 16;
+    const int pt = kernel_tiles((npos_ + 15) / 16);
+    const int fpad = kernel_filters(d.cnn_filter_size, (npos_ + 15) / 16);
     if (d.input_rows > 32 || npos_ >= 1024) { fail("board too large"); return nullptr; }
     const bool v2 = d.resnet_v2 != 0;
     KernelChoice kc = select_kernel(fpad, pt, vs, precision, v2);
@@ -359,6 +360,102 @@ struct Layout {
     size_t off = 0;
     size_t alloc(size_t bytes) { size_t o = off; off = (off + bytes + 255) & ~(size_t)255; return o; }
 };
+
+// The device weight image: byte offsets of every packed tensor (one allocation), the same for the
+// host packing (gz_net_set_weights) and the device one (gz_net_set_weights_device)
+struct ImageLayout {
+    size_t w0, w0lo, b0, wres, bres, wh, bh, wcl, bcl, pd[GZ_MAX_ROLES], pb[GZ_MAX_ROLES], vhw, vhb, pre, sew1, sew2, vdw,
+        vdb, pdp[GZ_MAX_ROLES] = {}, total;
+    // element counts
+    size_t n_w0, n_wres, n_wh, n_wcl, n_pd[GZ_MAX_ROLES], n_vhw, n_pre, n_sew1, n_sew2, n_pdp[GZ_MAX_ROLES] = {};
+};
+
+ImageLayout image_layout(const gz_net* net) {
+    const gz_net_desc& d = net->d;
+    const int FP = net->fpad, B = d.residual_layers, R = d.role_count, P2 = net->p2, S = d.se_units;
+    const int HW = d.input_columns * d.input_rows, HC = 2 * R + 1, NL = cal_layers(d);
+    const int VH = d.value_hidden_size, VK = value_features(d);
+    ImageLayout I;
+    I.n_w0 = (size_t)net->K0 * FP;
+    I.n_wres = (size_t)P2 * 2 * B * 9 * FP * FP;
+    I.n_wh = (size_t)HC * FP;
+    I.n_wcl = (size_t)std::max(NL, 1) * FP;
+    for (int r = 0; r < R; ++r) I.n_pd[r] = (size_t)2 * HW * ((d.policy_dist_count[r] + 3) & ~3);
+    I.n_vhw = (size_t)VK * ((VH + 3) & ~3);
+    I.n_pre = d.resnet_v2 ? (size_t)2 * B * FP : 1;
+    I.n_sew1 = S ? (size_t)B * FP * S : 1;
+    I.n_sew2 = S ? (size_t)B * S * FP : 1;
+    Layout L;
+    I.w0 = L.alloc(I.n_w0 * 2);
+    I.w0lo = L.alloc((P2 == 2 ? I.n_w0 : 1) * 2);
+    I.b0 = L.alloc((size_t)FP * 4);
+    I.wres = L.alloc(I.n_wres * 2);
+    I.bres = L.alloc((size_t)2 * B * FP * 4);
+    I.wh = L.alloc(I.n_wh * 4);
+    I.bh = L.alloc((size_t)HC * 4);
+    I.wcl = L.alloc(I.n_wcl * 4);
+    I.bcl = L.alloc((size_t)std::max(NL, 1) * 4);
+    for (int r = 0; r < R; ++r) {
+        I.pd[r] = L.alloc(I.n_pd[r] * 4);
+        I.pb[r] = L.alloc((size_t)d.policy_dist_count[r] * 4);
+    }
+    I.vhw = L.alloc(I.n_vhw * 4);
+    I.vhb = L.alloc((size_t)VH * 4);
+    I.pre = L.alloc(I.n_pre * 4);
+    I.sew1 = L.alloc(I.n_sew1 * 4);
+    I.sew2 = L.alloc(I.n_sew2 * 4);
+    I.vdw = L.alloc((size_t)VH * d.num_values * 4);
+    I.vdb = L.alloc((size_t)d.num_values * 4);
+    if (net->gemm_heads) {
+        const int nkt = (2 * HW + 31) / 32;
+        for (int r = 0; r < R; ++r) {
+            I.n_pdp[r] = (size_t)((d.policy_dist_count[r] + 15) / 16) * nkt * 2 * 64 * 8;
+            I.pdp[r] = L.alloc(I.n_pdp[r] * 2);
+        }
+    }
+    I.total = L.off;
+    return I;
+}
+
+// Swaps in the device image m (laid out by I) under the lock launch_segments takes, so a launcher
+// thread running a generation roll sees either the old or the new image, never a mix; the replaced
+// image is freed after a device sync (launches already queued may still read it).
+int install_image(gz_net* net, char* m, const ImageLayout& I) {
+    const int R = net->d.role_count;
+    std::unique_lock<std::mutex> wl(net->wmu);
+    char* old = net->dmem;
+    net->dmem = m;
+    KParams& kp = net->kp;
+    kp.w0 = (const __bf16*)(m + I.w0);
+    kp.w0lo = (const __bf16*)(m + I.w0lo);
+    kp.b0 = (const float*)(m + I.b0);
+    kp.wres = (const __bf16*)(m + I.wres);
+    kp.bres = (const float*)(m + I.bres);
+    kp.wh = (const float*)(m + I.wh);
+    kp.bh = (const float*)(m + I.bh);
+    kp.wcl = (const float*)(m + I.wcl);
+    kp.bcl = (const float*)(m + I.bcl);
+    for (int r = 0; r < R; ++r) {
+        kp.pd[r] = (const float*)(m + I.pd[r]);
+        kp.pb[r] = (const float*)(m + I.pb[r]);
+    }
+    kp.vhw = (const float*)(m + I.vhw);
+    kp.vhb = (const float*)(m + I.vhb);
+    kp.vdw = (const float*)(m + I.vdw);
+    kp.vdb = (const float*)(m + I.vdb);
+    kp.pre = (const float*)(m + I.pre);
+    kp.sew1 = (const float*)(m + I.sew1);
+    kp.sew2 = (const float*)(m + I.sew2);
+    for (int r = 0; r < R; ++r) kp.pdp[r] = net->gemm_heads ? (const __bf16*)(m + I.pdp[r]) : nullptr;
+    net->has_weights = true;
+    net->image_bytes = I.total;
+    wl.unlock();
+    if (old) {
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipFree(old));
+    }
+    return 0;
+}
 }  // namespace
 
 extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) {
@@ -532,25 +629,11 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
     for (int r = 0; r < R; ++r) pdq[r] = pad4(pdense[r], 2 * HW, d.policy_dist_count[r]);
     const std::vector<float> vhq = pad4(vhw, VK, d.value_hidden_size);
 
-    // device layout
-    Layout L;
-    const size_t o_w0 = L.alloc(w0.size() * 2), o_w0lo = L.alloc(std::max<size_t>(w0lo.size(), 1) * 2);
-    const size_t o_b0 = L.alloc(b0.size() * 4);
-    const size_t o_wres = L.alloc(wres.size() * 2), o_bres = L.alloc(bres.size() * 4);
-    const size_t o_wh = L.alloc(wh.size() * 4), o_bh = L.alloc(bh.size() * 4);
-    const size_t o_wcl = L.alloc(wcl.size() * 4), o_bcl = L.alloc(bcl.size() * 4);
-    size_t o_pd[GZ_MAX_ROLES], o_pb[GZ_MAX_ROLES];
-    for (int r = 0; r < R; ++r) {
-        o_pd[r] = L.alloc(pdq[r].size() * 4);
-        o_pb[r] = L.alloc((size_t)d.policy_dist_count[r] * 4);
-    }
-    const size_t o_vhw = L.alloc(vhq.size() * 4), o_vhb = L.alloc(d.value_hidden_size * 4);
-    const size_t o_pre = L.alloc(pre.size() * 4), o_sew1 = L.alloc(sew1.size() * 4), o_sew2 = L.alloc(sew2.size() * 4);
-    const size_t o_vdw = L.alloc((size_t)d.value_hidden_size * d.num_values * 4), o_vdb = L.alloc(d.num_values * 4);
+    // device layout (image_layout: the same offsets as the device packing's)
+    const ImageLayout I = image_layout(net);
     // policy_gemm_kernel's A fragments: W^T tiles [jt][kt][hi | lo][64 lanes][8 k] bf16, lane l holding
     // row j = 16 jt + l % 16 and k = 32 kt + 8 (l / 16) + e (zero padded)
     std::vector<std::vector<uint16_t>> pdp(R);
-    size_t o_pdp[GZ_MAX_ROLES] = {};
     if (net->gemm_heads) {
         const int K = 2 * HW, nkt = (K + 31) / 32;
         for (int r = 0; r < R; ++r) {
@@ -567,84 +650,392 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
                             pdp[r][o] = f2bf(v);
                             pdp[r][o + 64 * 8] = lo_of(v);
                         }
-            o_pdp[r] = L.alloc(pdp[r].size() * 2);
         }
     }
 
-    std::vector<char> img(L.off, 0);
+    std::vector<char> img(I.total, 0);
     auto put = [&](size_t off, const void* src, size_t bytes) { std::memcpy(img.data() + off, src, bytes); };
-    put(o_w0, w0.data(), w0.size() * 2);
-    if (P2 == 2) put(o_w0lo, w0lo.data(), w0lo.size() * 2);
-    put(o_b0, b0.data(), b0.size() * 4);
-    put(o_wres, wres.data(), wres.size() * 2);
-    put(o_bres, bres.data(), bres.size() * 4);
-    put(o_wh, wh.data(), wh.size() * 4);
-    put(o_bh, bh.data(), bh.size() * 4);
-    put(o_wcl, wcl.data(), wcl.size() * 4);
-    put(o_bcl, bcl.data(), bcl.size() * 4);
+    put(I.w0, w0.data(), w0.size() * 2);
+    if (P2 == 2) put(I.w0lo, w0lo.data(), w0lo.size() * 2);
+    put(I.b0, b0.data(), b0.size() * 4);
+    put(I.wres, wres.data(), wres.size() * 2);
+    put(I.bres, bres.data(), bres.size() * 4);
+    put(I.wh, wh.data(), wh.size() * 4);
+    put(I.bh, bh.data(), bh.size() * 4);
+    put(I.wcl, wcl.data(), wcl.size() * 4);
+    put(I.bcl, bcl.data(), bcl.size() * 4);
     for (int r = 0; r < R; ++r) {
-        put(o_pd[r], pdq[r].data(), pdq[r].size() * 4);   // Keras [2HW][P_r] (k-major), rows padded to P4
-        put(o_pb[r], pbias[r], (size_t)d.policy_dist_count[r] * 4);
+        put(I.pd[r], pdq[r].data(), pdq[r].size() * 4);   // Keras [2HW][P_r] (k-major), rows padded to P4
+        put(I.pb[r], pbias[r], (size_t)d.policy_dist_count[r] * 4);
     }
-    put(o_vhw, vhq.data(), vhq.size() * 4);   // Keras [VK][VH], rows padded to VH4
-    put(o_pre, pre.data(), pre.size() * 4);
-    put(o_sew1, sew1.data(), sew1.size() * 4);
-    put(o_sew2, sew2.data(), sew2.size() * 4);
-    put(o_vhb, vhb, d.value_hidden_size * 4);
-    put(o_vdw, vdw, (size_t)d.value_hidden_size * d.num_values * 4);
-    put(o_vdb, vdb, d.num_values * 4);
+    put(I.vhw, vhq.data(), vhq.size() * 4);   // Keras [VK][VH], rows padded to VH4
+    put(I.pre, pre.data(), pre.size() * 4);
+    put(I.sew1, sew1.data(), sew1.size() * 4);
+    put(I.sew2, sew2.data(), sew2.size() * 4);
+    put(I.vhb, vhb, d.value_hidden_size * 4);
+    put(I.vdw, vdw, (size_t)d.value_hidden_size * d.num_values * 4);
+    put(I.vdb, vdb, d.num_values * 4);
     if (net->gemm_heads)
-        for (int r = 0; r < R; ++r) put(o_pdp[r], pdp[r].data(), pdp[r].size() * 2);
+        for (int r = 0; r < R; ++r) put(I.pdp[r], pdp[r].data(), pdp[r].size() * 2);
 
     HIPCHK(hipSetDevice(net->device));
     char* m = nullptr;
-    HIPCHK(hipMalloc((void**)&m, L.off));
-    if (hipMemcpy(m, img.data(), L.off, hipMemcpyHostToDevice) != hipSuccess) {
+    HIPCHK(hipMalloc((void**)&m, I.total));
+    if (hipMemcpy(m, img.data(), I.total, hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(m);
         return fail("weight upload failed");
     }
-    // swap under the lock launch_segments takes: a launcher thread running a generation roll sees
-    // either the old or the new image, never a mix
-    std::unique_lock<std::mutex> wl(net->wmu);
-    char* old = net->dmem;
-    net->dmem = m;
-    KParams& kp = net->kp;
-    kp.w0 = (const __bf16*)(m + o_w0);
-    kp.w0lo = (const __bf16*)(m + o_w0lo);
-    kp.b0 = (const float*)(m + o_b0);
-    kp.wres = (const __bf16*)(m + o_wres);
-    kp.bres = (const float*)(m + o_bres);
-    kp.wh = (const float*)(m + o_wh);
-    kp.bh = (const float*)(m + o_bh);
-    kp.wcl = (const float*)(m + o_wcl);
-    kp.bcl = (const float*)(m + o_bcl);
-    for (int r = 0; r < R; ++r) {
-        kp.pd[r] = (const float*)(m + o_pd[r]);
-        kp.pb[r] = (const float*)(m + o_pb[r]);
-    }
-    kp.vhw = (const float*)(m + o_vhw);
-    kp.vhb = (const float*)(m + o_vhb);
-    kp.vdw = (const float*)(m + o_vdw);
-    kp.vdb = (const float*)(m + o_vdb);
-    kp.pre = (const float*)(m + o_pre);
-    kp.sew1 = (const float*)(m + o_sew1);
-    kp.sew2 = (const float*)(m + o_sew2);
-    for (int r = 0; r < R; ++r) kp.pdp[r] = net->gemm_heads ? (const __bf16*)(m + o_pdp[r]) : nullptr;
-    net->has_weights = true;
-    wl.unlock();
-    if (old) {   // launches already queued may still read the old image
-        HIPCHK(hipDeviceSynchronize());
-        HIPCHK(hipFree(old));
-    }
-    return 0;
+    return install_image(net, m, I);
 }
+
+// ---- the same packing on the device (generation roll: the blob arrives in HBM by an RCCL broadcast)
+// Every value is computed with the host path's operations and rounding (correctly rounded divide /
+// sqrt, no contraction, the same bf16 rounding), so the two images are byte-identical
+// (tests/test_weight_roll_gpu.py); only the offsets of the blob's tensors are walked on the host.
+namespace {
+struct BNRef {                  // a BatchNorm over n channels after a conv with optional bias cb
+    const float *g = nullptr, *be = nullptr, *mu = nullptr, *var = nullptr, *cb = nullptr;
+    int n = 0;                  // g == nullptr: no BN (scale 1, bias cb or 0)
+    int out = 0;                // offset of its scale[n] | bias[n] in the fold buffer
+};
+struct BlobPlan {
+    const float* w0 = nullptr;
+    BNRef bn0;
+    std::vector<const float*> wconv;   // [2B] 3x3 conv kernels
+    std::vector<BNRef> bnconv;         // [2B] the BN folded into each
+    std::vector<BNRef> pre;            // v2: [B] the block's first BN (scale / shift of the stream)
+    std::vector<const float*> se_c, se_g;
+    const float* hw[GZ_MAX_ROLES] = {};
+    BNRef hbn[GZ_MAX_ROLES];
+    const float* pd[GZ_MAX_ROLES] = {};
+    const float* pb[GZ_MAX_ROLES] = {};
+    std::vector<const float*> clw;
+    std::vector<BNRef> clbn;
+    const float* vw = nullptr;
+    BNRef vbn;
+    const float *vhw = nullptr, *vhb = nullptr, *vdw = nullptr, *vdb = nullptr;
+    size_t consumed = 0;
+    int fold_floats = 0;
+};
+
+// the tensors of the canonical blob at base (desc.py weight_spec; the order gz_net_set_weights reads)
+BlobPlan blob_plan(const gz_net_desc& d, const float* base) {
+    BlobPlan P;
+    Cursor cur{base};
+    const int F = d.cnn_filter_size, C = d.input_channels, B = d.residual_layers, R = d.role_count, S = d.se_units;
+    const int HW = d.input_columns * d.input_rows, k0 = initial_kernel(d), NL = cal_layers(d);
+    auto cbias = [&](int n) -> const float* { return d.conv_bias ? cur.take(n) : nullptr; };
+    auto bn = [&](int n, const float* cb) {
+        BNRef b;
+        b.g = cur.take(n); b.be = cur.take(n); b.mu = cur.take(n); b.var = cur.take(n);
+        b.cb = cb; b.n = n; b.out = P.fold_floats;
+        P.fold_floats += 2 * n;
+        return b;
+    };
+    auto nobn = [&](int n, const float* cb) {
+        BNRef b;
+        b.cb = cb; b.n = n; b.out = P.fold_floats;
+        P.fold_floats += 2 * n;
+        return b;
+    };
+    P.w0 = cur.take((size_t)k0 * k0 * C * F);
+    {
+        const float* cb = cbias(F);
+        P.bn0 = has_initial_bn(d) ? bn(F, cb) : nobn(F, cb);
+    }
+    for (int blk = 0; blk < B; ++blk) {
+        if (!d.resnet_v2) {
+            for (int j = 0; j < 2; ++j) {
+                P.wconv.push_back(cur.take((size_t)9 * F * F));
+                const float* cb = cbias(F);
+                P.bnconv.push_back(bn(F, cb));
+            }
+            continue;
+        }
+        P.pre.push_back(bn(F, nullptr));
+        P.wconv.push_back(cur.take((size_t)9 * F * F));
+        {
+            const float* cb = cbias(F);
+            P.bnconv.push_back(bn(F, cb));
+        }
+        P.wconv.push_back(cur.take((size_t)9 * F * F));
+        P.bnconv.push_back(nobn(F, cbias(F)));
+        if (S) {
+            P.se_c.push_back(cur.take((size_t)F * S));
+            P.se_g.push_back(cur.take((size_t)S * F));
+        }
+    }
+    for (int r = 0; r < R; ++r) {
+        P.hw[r] = cur.take((size_t)F * 2);
+        const float* cb = cbias(2);
+        P.hbn[r] = bn(2, cb);
+        P.pd[r] = cur.take((size_t)2 * HW * d.policy_dist_count[r]);
+        P.pb[r] = cur.take(d.policy_dist_count[r]);
+    }
+    for (int j = 0; j < NL; ++j) {
+        P.clw.push_back(cur.take(F));
+        const float* cb = cbias(1);
+        P.clbn.push_back(bn(1, cb));
+    }
+    if (NL == 0) {
+        P.vw = cur.take(F);
+        const float* cb = cbias(1);
+        P.vbn = d.value_bn ? bn(1, cb) : nobn(1, cb);
+    }
+    P.vhw = cur.take((size_t)value_features(d) * d.value_hidden_size);
+    P.vhb = cur.take(d.value_hidden_size);
+    P.vdw = cur.take((size_t)d.value_hidden_size * d.num_values);
+    P.vdb = cur.take(d.num_values);
+    P.consumed = (size_t)(cur.p - base);
+    return P;
+}
+
+// Float operations with the host's rounding whatever the device compiler contracts or approximates:
+// each computed in double and rounded to float at once -- correctly rounded, since 53 >= 2 x 24 + 2
+// bits makes the double rounding innocuous for + - * / sqrt.  The opaque register barriers keep the
+// compiler from narrowing the double operation back to a float one and from fusing a multiply with
+// the next add into one v_fma_f32 (which -ffp-contract=fast would otherwise do: observed as 1-5 ulp
+// differences of the folded biases from the host's).
+__device__ __forceinline__ double f_keep(double x) { asm volatile("" : "+v"(x)); return x; }
+__device__ __forceinline__ float f_keep(float x) { asm volatile("" : "+v"(x)); return x; }
+__device__ __forceinline__ float f_mul(float a, float b) { return f_keep((float)f_keep((double)a * (double)b)); }
+__device__ __forceinline__ float f_add(float a, float b) { return f_keep((float)f_keep((double)a + (double)b)); }
+__device__ __forceinline__ float f_sub(float a, float b) { return f_keep((float)f_keep((double)a - (double)b)); }
+__device__ __forceinline__ float f_div(float a, float b) { return f_keep((float)f_keep(__ddiv_rn((double)a, (double)b))); }
+__device__ __forceinline__ float f_sqrt(float a) { return f_keep((float)f_keep(__dsqrt_rn((double)a))); }
+
+__device__ __forceinline__ uint16_t lo_of_dev(float v) {
+    const uint16_t h = f2bf(v);
+    return f2bf(f_sub(v, __builtin_bit_cast(float, (uint32_t)h << 16)));
+}
+
+struct BNJob {
+    const float *g, *be, *mu, *var, *cb;
+    int n, out;
+};
+// scale = g / sqrt(var + eps), bias = be - mu scale (with a conv bias: be + (cb - mu) scale); no BN:
+// scale 1, bias cb or 0 -- gz_net_set_weights' bn_fold, operation for operation
+__global__ void bn_fold_kernel(const BNJob* jobs, float* fold) {
+    const BNJob j = jobs[blockIdx.x];
+    for (int i = threadIdx.x; i < j.n; i += blockDim.x) {
+        float sc = 1.f, bi = j.cb ? j.cb[i] : 0.f;
+        if (j.g) {
+            sc = f_div(j.g[i], f_sqrt(f_add(j.var[i], 1e-3f)));
+            bi = j.cb ? f_add(j.be[i], f_mul(f_sub(j.cb[i], j.mu[i]), sc)) : f_sub(j.be[i], f_mul(j.mu[i], sc));
+        }
+        fold[j.out + i] = sc;
+        fold[j.out + j.n + i] = bi;
+    }
+}
+
+// one trunk conv [3][3][F][F] * scale[co] -> [tap][kc][co][P2 x 32] bf16 (+ its bias row)
+__global__ void pack_conv_kernel(const float* w, const float* scale, const float* bias, uint16_t* dst, float* bres,
+                                 int F, int FP, int P2) {
+    const size_t n = (size_t)9 * F * F;
+    const int KC = FP / 32;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int co = (int)(i % F), ci = (int)((i / F) % F), tap = (int)(i / ((size_t)F * F));
+        const float v = f_mul(w[i], scale[co]);
+        const size_t o = ((((size_t)tap * KC + ci / 32) * FP + co) * P2) * 32 + (ci % 32);
+        dst[o] = f2bf(v);
+        if (P2 == 2) dst[o + 32] = lo_of_dev(v);
+        if (tap == 0 && ci == 0) bres[co] = bias[co];
+    }
+}
+
+// initial conv [k0][k0][C][F] -> [K0 / 32][FP][32], k = tap C + c (hi; lo for split precision)
+__global__ void pack_w0_kernel(const float* w, const float* scale, const float* bias, uint16_t* w0, uint16_t* w0lo,
+                               float* b0, int KF, int F, int FP) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < KF; i += gridDim.x * blockDim.x) {
+        const int k = i / F, co = i % F;
+        const float v = f_mul(w[i], scale[co]);
+        const size_t o = ((size_t)(k / 32) * FP + co) * 32 + (k % 32);
+        w0[o] = f2bf(v);
+        if (w0lo) w0lo[o] = lo_of_dev(v);
+        if (k == 0) b0[co] = bias[co];
+    }
+}
+
+// dst[i ds] = src[i ss] (mode 0), * sc[i] (1), * sc[0] (2)
+struct VecJob {
+    const float* src;
+    float* dst;
+    const float* sc;
+    int n, ss, ds, mode;
+};
+__global__ void vec_kernel(const VecJob* jobs) {
+    const VecJob j = jobs[blockIdx.x];
+    for (int i = threadIdx.x; i < j.n; i += blockDim.x) {
+        const float v = j.src[(size_t)i * j.ss];
+        j.dst[(size_t)i * j.ds] = j.mode == 0 ? v : f_mul(v, j.mode == 1 ? j.sc[i] : j.sc[0]);
+    }
+}
+
+// policy_gemm_kernel's A fragments of one role (the host path's pdp loop)
+__global__ void pack_pdp_kernel(const float* pd, uint16_t* dst, int P, int K, int nkt, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int e = (int)(i % 8), l = (int)((i / 8) % 64);
+        const size_t t = i / (8 * 64);      // jt * nkt + kt
+        const int kt = (int)(t % nkt), jt = (int)(t / nkt);
+        const int j = 16 * jt + (l & 15), k = 32 * kt + 8 * (l >> 4) + e;
+        if (j >= P || k >= K) continue;
+        const float v = pd[(size_t)k * P + j];
+        const size_t o = ((t * 2) * 64 + l) * 8 + e;
+        dst[o] = f2bf(v);
+        dst[o + 64 * 8] = lo_of_dev(v);
+    }
+}
+}  // namespace
 
 extern "C" int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_t count) {
     if (!net || !d_blob) return fail("null argument");
-    std::vector<float> h(count);
+    if (count != net->nweights)
+        return fail("weight count mismatch: got " + std::to_string(count) + " expected " + std::to_string(net->nweights));
+    if (getenv("GZ_HOST_WEIGHT_ROLL")) {   // diagnostics: the round-trip path (D2H, host fold / pack, H2D)
+        std::vector<float> h(count);
+        HIPCHK(hipSetDevice(net->device));
+        HIPCHK(hipMemcpy(h.data(), d_blob, count * 4, hipMemcpyDeviceToHost));
+        return gz_net_set_weights(net, h.data(), count);
+    }
+    const gz_net_desc& d = net->d;
+    const int F = d.cnn_filter_size, FP = net->fpad, B = d.residual_layers, R = d.role_count, S = d.se_units;
+    const int HW = d.input_columns * d.input_rows, P2 = net->p2, NL = cal_layers(d);
+    const int VH = d.value_hidden_size, VK = value_features(d);
+    const BlobPlan P = blob_plan(d, d_blob);
+    if (P.consumed != count) return fail("internal: blob plan mismatch");
+    const ImageLayout I = image_layout(net);
     HIPCHK(hipSetDevice(net->device));
-    HIPCHK(hipMemcpy(h.data(), d_blob, count * 4, hipMemcpyDeviceToHost));
-    return gz_net_set_weights(net, h.data(), count);
+    hipStream_t st = net->stream;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, st));
+    char* m = nullptr;
+    float* fold = nullptr;
+    void* jobs_d = nullptr;
+    auto cleanup = [&]() {
+        if (fold) (void)hipFree(fold);
+        if (jobs_d) (void)hipFree(jobs_d);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    };
+    auto bail = [&](const std::string& what, hipError_t e) {
+        cleanup();
+        if (m) (void)hipFree(m);
+        return fail(what + ": " + hipGetErrorString(e));
+    };
+    hipError_t e;
+    if ((e = hipMalloc((void**)&m, I.total)) != hipSuccess) return bail("hipMalloc image", e);
+    if ((e = hipMalloc((void**)&fold, (size_t)std::max(P.fold_floats, 1) * 4)) != hipSuccess) return bail("hipMalloc fold", e);
+    if ((e = hipMemsetAsync(m, 0, I.total, st)) != hipSuccess) return bail("hipMemsetAsync", e);
+
+    // BN folds (every BNRef of the plan)
+    std::vector<BNJob> bj;
+    auto addbn = [&](const BNRef& b) { bj.push_back(BNJob{b.g, b.be, b.mu, b.var, b.cb, b.n, b.out}); };
+    addbn(P.bn0);
+    for (const BNRef& b : P.bnconv) addbn(b);
+    for (const BNRef& b : P.pre) addbn(b);
+    for (int r = 0; r < R; ++r) addbn(P.hbn[r]);
+    for (const BNRef& b : P.clbn) addbn(b);
+    if (NL == 0) addbn(P.vbn);
+    // the small vectors derived from the folds (heads' 1x1 convs, per-layer value convs, v2 pre-BN)
+    std::vector<VecJob> vj;
+    auto sc_of = [&](const BNRef& b) { return fold + b.out; };
+    auto bi_of = [&](const BNRef& b) { return fold + b.out + b.n; };
+    char* const mc = m;
+    float* wh = (float*)(mc + I.wh);
+    float* bh = (float*)(mc + I.bh);
+    for (int r = 0; r < R; ++r)
+        for (int c = 0; c < 2; ++c) {
+            vj.push_back(VecJob{P.hw[r] + c, wh + (size_t)(2 * r + c) * FP, sc_of(P.hbn[r]) + c, F, 2, 1, 2});
+            vj.push_back(VecJob{bi_of(P.hbn[r]) + c, bh + 2 * r + c, nullptr, 1, 1, 1, 0});
+        }
+    for (int j = 0; j < NL; ++j) {
+        vj.push_back(VecJob{P.clw[j], (float*)(mc + I.wcl) + (size_t)j * FP, sc_of(P.clbn[j]), F, 1, 1, 2});
+        vj.push_back(VecJob{bi_of(P.clbn[j]), (float*)(mc + I.bcl) + j, nullptr, 1, 1, 1, 0});
+    }
+    if (NL == 0) {
+        vj.push_back(VecJob{P.vw, wh + (size_t)(2 * R) * FP, sc_of(P.vbn), F, 1, 1, 2});
+        vj.push_back(VecJob{bi_of(P.vbn), bh + 2 * R, nullptr, 1, 1, 1, 0});
+    }
+    for (int blk = 0; blk < (int)P.pre.size(); ++blk) {
+        vj.push_back(VecJob{sc_of(P.pre[blk]), (float*)(mc + I.pre) + (size_t)(2 * blk) * FP, nullptr, F, 1, 1, 0});
+        vj.push_back(VecJob{bi_of(P.pre[blk]), (float*)(mc + I.pre) + (size_t)(2 * blk + 1) * FP, nullptr, F, 1, 1, 0});
+    }
+    const size_t bj_bytes = bj.size() * sizeof(BNJob), vj_bytes = vj.size() * sizeof(VecJob);
+    if ((e = hipMalloc(&jobs_d, bj_bytes + vj_bytes + 16)) != hipSuccess) return bail("hipMalloc jobs", e);
+    BNJob* bj_d = (BNJob*)jobs_d;
+    VecJob* vj_d = (VecJob*)((char*)jobs_d + ((bj_bytes + 15) & ~(size_t)15));
+    if ((e = hipMemcpyAsync(bj_d, bj.data(), bj_bytes, hipMemcpyHostToDevice, st)) != hipSuccess) return bail("jobs", e);
+    if (!vj.empty() && (e = hipMemcpyAsync(vj_d, vj.data(), vj_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
+        return bail("jobs", e);
+    hipLaunchKernelGGL(bn_fold_kernel, dim3((unsigned)bj.size()), dim3(256), 0, st, bj_d, fold);
+    {   // initial conv
+        const int KF = initial_kernel(d) * initial_kernel(d) * d.input_channels * F;
+        hipLaunchKernelGGL(pack_w0_kernel, dim3((KF + 255) / 256), dim3(256), 0, st, P.w0, sc_of(P.bn0), bi_of(P.bn0),
+                           (uint16_t*)(mc + I.w0), P2 == 2 ? (uint16_t*)(mc + I.w0lo) : (uint16_t*)nullptr,
+                           (float*)(mc + I.b0), KF, F, FP);
+    }
+    for (int c = 0; c < 2 * B; ++c) {
+        const size_t n = (size_t)9 * F * F;
+        hipLaunchKernelGGL(pack_conv_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
+                           P.wconv[c], sc_of(P.bnconv[c]), bi_of(P.bnconv[c]),
+                           (uint16_t*)(mc + I.wres) + (size_t)P2 * c * 9 * FP * FP, (float*)(mc + I.bres) + (size_t)c * FP,
+                           F, FP, P2);
+    }
+    if (!vj.empty()) hipLaunchKernelGGL(vec_kernel, dim3((unsigned)vj.size()), dim3(256), 0, st, vj_d);
+    // plain copies: the dense heads (output dimension padded to 4), biases, squeeze-excite layers
+    auto cp = [&](void* dst, const void* src, size_t bytes) { return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st); };
+    auto cp2 = [&](void* dst, size_t dpitch, const void* src, size_t spitch, size_t w, size_t h) {
+        return hipMemcpy2DAsync(dst, dpitch, src, spitch, w, h, hipMemcpyDeviceToDevice, st);
+    };
+    for (int r = 0; r < R; ++r) {
+        const int Pr = d.policy_dist_count[r];
+        if ((e = cp2(mc + I.pd[r], (size_t)((Pr + 3) & ~3) * 4, P.pd[r], (size_t)Pr * 4, (size_t)Pr * 4, (size_t)2 * HW)) != hipSuccess)
+            return bail("policy dense", e);
+        if ((e = cp(mc + I.pb[r], P.pb[r], (size_t)Pr * 4)) != hipSuccess) return bail("policy bias", e);
+    }
+    if ((e = cp2(mc + I.vhw, (size_t)((VH + 3) & ~3) * 4, P.vhw, (size_t)VH * 4, (size_t)VH * 4, (size_t)VK)) != hipSuccess)
+        return bail("value dense", e);
+    if ((e = cp(mc + I.vhb, P.vhb, (size_t)VH * 4)) != hipSuccess) return bail("value bias", e);
+    if ((e = cp(mc + I.vdw, P.vdw, (size_t)VH * d.num_values * 4)) != hipSuccess) return bail("value out", e);
+    if ((e = cp(mc + I.vdb, P.vdb, (size_t)d.num_values * 4)) != hipSuccess) return bail("value out bias", e);
+    for (int blk = 0; blk < (int)P.se_c.size(); ++blk) {
+        if ((e = cp((float*)(mc + I.sew1) + (size_t)blk * FP * S, P.se_c[blk], (size_t)F * S * 4)) != hipSuccess)
+            return bail("squeeze-excite", e);
+        if ((e = cp2((float*)(mc + I.sew2) + (size_t)blk * S * FP, (size_t)FP * 4, P.se_g[blk], (size_t)F * 4, (size_t)F * 4,
+                     (size_t)S)) != hipSuccess)
+            return bail("squeeze-excite", e);
+    }
+    if (net->gemm_heads) {
+        const int K = 2 * HW, nkt = (K + 31) / 32;
+        for (int r = 0; r < R; ++r) {
+            const size_t n = I.n_pdp[r] / 2;   // (hi, lo) pairs
+            hipLaunchKernelGGL(pack_pdp_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
+                               P.pd[r], (uint16_t*)(mc + I.pdp[r]), d.policy_dist_count[r], K, nkt, n);
+        }
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return bail("pack kernels", e);
+    if ((e = hipEventRecord(e1, st)) != hipSuccess || (e = hipStreamSynchronize(st)) != hipSuccess) return bail("roll sync", e);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    net->last_roll_ms = ms;
+    cleanup();
+    return install_image(net, m, I);
+}
+
+extern "C" double gz_net_last_roll_ms(const gz_net* net) { return net ? (double)net->last_roll_ms : -1.0; }
+
+// diagnostics: the device weight image (out == NULL: its size)
+extern "C" size_t gz_net_copy_weight_image(gz_net* net, void* out, size_t cap) {
+    if (!net || !net->dmem) return 0;
+    std::lock_guard<std::mutex> wl(net->wmu);
+    if (!out) return net->image_bytes;
+    const size_t n = std::min(cap, net->image_bytes);
+    if (hipSetDevice(net->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, net->dmem, n, hipMemcpyDeviceToHost) != hipSuccess)
+        return 0;
+    return n;
 }
 
 static int launch_segments(gz_net* net, hipStream_t stream, const gz_segment* segs, int nseg,

@@ -147,6 +147,7 @@ struct gz_runner {
     std::string roll_err;
     std::vector<long> roll_batches;  // per pool: batches launched on the previous network
     long roll_launches = 0;          // launches issued on the previous network
+    double roll_apply_ms = 0.0;      // the launcher's wall time applying the last roll
 };
 
 static void set_failed(gz_runner* r, const std::string& msg) {
@@ -245,8 +246,10 @@ static void engine_main(gz_runner* r, int tid) {
 // launcher swaps it between two launches.  gz_net_set_weights waits for the launches in flight
 // (which finish on the previous image) before freeing it.
 static void apply_roll(gz_runner* r, long launches_issued) {
+    const auto t0 = std::chrono::steady_clock::now();
     const int rc = r->roll_device ? gz_net_set_weights_device(r->net, r->roll_blob, r->roll_count)
                                   : gz_net_set_weights(r->net, r->roll_blob, r->roll_count);
+    r->roll_apply_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     int rc2 = 0;
     if (rc == 0 && r->roll_clear) {
         if (r->shared_unique) {
@@ -864,7 +867,9 @@ extern "C" int gz_runner_update_network(gz_runner* r, const float* blob, size_t 
         return 0;
     }
     std::unique_lock<std::mutex> lk(r->roll_m);
-    if (r->roll_state.load() == 1) {
+    // one caller at a time: any state but 0 means another caller owns the roll (pending, being
+    // applied, or applied / failed and not yet collected -- that caller resets it to 0 on return)
+    if (r->roll_state.load() != 0) {
         g_err = "a generation roll is already pending";
         return -1;
     }
@@ -915,6 +920,8 @@ extern "C" int gz_runner_ordinal_stats(gz_runner* r, gz_ordinal_stats* out) {
         }
     return 0;
 }
+
+extern "C" double gz_runner_roll_apply_ms(gz_runner* r) { return r ? r->roll_apply_ms : -1.0; }
 
 // After gz_runner_update_network: per pool, the batches launched on the previous network (the
 // pool's batches 0 .. pool_batches[i]-1 ran on it, the later ones on the new one), and the launches

@@ -15,6 +15,7 @@ KernelChoice trunk_variant_f128(int pt, int v, int precision) {
         case 9: return variants<128, 9>(v, precision);
         case 10: return variants<128, 10>(v, precision);
         case 11: return variants<128, 11>(v, precision);
+        case 23: return variants<128, 23>(v, precision);   // 19 x 19
         default: return KernelChoice{};
     }
 }

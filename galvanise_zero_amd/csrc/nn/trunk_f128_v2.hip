@@ -15,6 +15,7 @@ KernelChoice trunk_variant_f128_v2(int pt, int v, int precision) {
         case 9: return variants<128, 9, true>(v, precision);
         case 10: return variants<128, 10, true>(v, precision);
         case 11: return variants<128, 11, true>(v, precision);
+        case 23: return variants<128, 23, true>(v, precision);   // 19 x 19
         default: return KernelChoice{};
     }
 }

@@ -82,6 +82,13 @@ KernelChoice variants(int v, int precision) {
             }
             return KernelChoice{};
         }
+        // F <= 128 on boards of more than 64 positions (up to 19 x 19): one board per workgroup in a
+        // single image with one part at a time -- the two-pass kernel (P = 2; at 19 x 19 the hi + lo
+        // image would need 201 KB), which also takes v2 nets (the reference's hexLG / hex19 files)
+        if constexpr (F <= 128 && PTN > 4) {
+            if (v == 11) return kernel_for<F, PTN, 1, 1, 2, V2>();
+            return KernelChoice{};
+        }
         if constexpr (F <= 128 && PTN <= 4) {
             if constexpr (2 * Geo<F, PTN, 1, 3>::ACT_BYTES + 16 * 1024 <= 160 * 1024) {
                 if (v == 11) return kernel_for<F, PTN, 1, 1, 3, V2>();
@@ -120,7 +127,16 @@ KernelChoice trunk_variant_f128_v2(int pt, int v, int precision);
 
 // padded filter count and position tiles of a board; 0 when not compiled
 inline int padded_filters(int F) { return F <= 64 ? 64 : F <= 128 ? 128 : F <= 256 ? 256 : 0; }
-constexpr int kMaxPT = 11;   // boards of up to 176 positions (13 x 13)
+constexpr int kMaxPT = 23;   // boards of up to 368 positions (19 x 19)
+// Boards beyond 13 x 13 run on the 23-tile kernels (19 x 19; smaller boards leave tiles off the
+// board, which read the zero rows and store nothing) with 128 filters (F <= 64 padded up: the
+// 64-filter rows are too narrow for the padded layout that fits a 19 x 19 image in the LDS).
+constexpr int kLargePT = 23;
+inline int kernel_tiles(int pt) { return pt > 11 && pt <= kLargePT ? kLargePT : pt; }
+inline int kernel_filters(int F, int pt) {
+    const int f = padded_filters(F);
+    return pt > 11 && f == 64 ? 128 : f;
+}
 
 inline KernelChoice trunk_variant(int fpad, int pt, int v, int precision, bool v2 = false) {
     if (v2) {

@@ -64,7 +64,11 @@ class SelfPlayRunner(object):
         pb = (ctypes.c_long * self.num_pools)()
         lb = ctypes.c_long()
         self.lib.gz_runner_roll_info(self.handle, pb, self.num_pools, ctypes.byref(lb))
-        return {"pool_batches": list(pb), "launches_before": lb.value}
+        # apply_ms: the launcher's wall time applying it (fold / pack / swap); device_ms: the fold +
+        # pack kernels of a device blob
+        return {"pool_batches": list(pb), "launches_before": lb.value,
+                "apply_ms": self.lib.gz_runner_roll_apply_ms(self.handle),
+                "device_ms": self.net.last_roll_ms() if dev else None}
 
     def wait_batches(self, total, timeout_s=600.0):
         rc = self.lib.gz_runner_wait_batches(self.handle, total, timeout_s)

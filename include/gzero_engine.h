@@ -217,6 +217,11 @@ int gz_engine_set_verify_fastpath(int on);
 long gz_engine_verified_decisions(void);
 char* gz_pool_fetch_samples_n(gz_pool* p, long* count);  /* as fetch_samples, *count = records */
 
+/* How this library was built (static string): "pgo=<use|none|stale|gen> march=<...>" -- use: gcc
+ * profiles recorded on these exact sources (csrc/pgo/sources.sha256); stale: profiles present but
+ * recorded on other sources, so not used.  Reported in the bench line. */
+const char* gz_engine_build_info(void);
+
 #ifdef __cplusplus
 }
 #endif

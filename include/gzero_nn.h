@@ -41,10 +41,12 @@ typedef struct gz_net_desc {
     int value_sigmoid;                        /* value Dense activation sigmoid (else softmax)      */
     /* Arithmetic of the residual trunk (build extension; the reference runs fp32 TF kernels):
      *   GZ_PRECISION_BF16 (0 or 1): bf16 operands, fp32 accumulation and residual stream;
-     *   GZ_PRECISION_SPLIT (3): fp32 accuracy -- each fp32 operand as bf16 hi + bf16 lo and each
-     *   product as hi*hi + hi*lo + lo*hi on the MFMA (~16 significant bits per operand, fp32
-     *   accumulation); F <= 128 on boards <= 64 positions, F = 256 on boards <= 13 x 13 (single
-     *   image; 13 x 13 by two passes per conv).  The heads' 1x1 convs, softmaxes and value MLP are
+     *   GZ_PRECISION_SPLIT (3): each fp32 operand as bf16 hi + bf16 lo and each product as
+     *   hi*hi + hi*lo + lo*hi on the MFMA (~16 significant bits per operand against fp32's 24, fp32
+     *   accumulation: pre-softmax logits within ~1e-4 relative of an fp32 forward, the per-config
+     *   bounds of nn/tolerance.py); F <= 128 on boards <= 64 positions two per workgroup, larger
+     *   boards (up to 19 x 19) one per workgroup, by two passes per conv where the hi + lo image
+     *   exceeds the LDS (F = 256 on 13 x 13, F = 128 on 19 x 19).  The heads' 1x1 convs, softmaxes and value MLP are
      *   fp32 in both modes; the policy Dense is fp32 except for single-image nets with a policy of
      *   >= 512 moves (amazons), whose policy Dense of the whole launch runs as one bf16x3 split MFMA
      *   GEMM in both modes (policy_gemm_kernel; GZ_NO_GEMM_HEADS=1 keeps it fp32 on the VALU).
@@ -81,8 +83,15 @@ size_t gz_net_weight_count(const gz_net* net);
  * weights, launches already in flight finish on the old ones, which are freed after a device sync. */
 int gz_net_set_weights(gz_net* net, const float* blob, size_t count);
 
-/* Upload weights from a *device* float32 blob (e.g. after an RCCL broadcast into device memory). */
+/* Upload weights from a *device* float32 blob (e.g. after an RCCL broadcast into device memory): the
+ * BN fold and the bf16 (hi / lo) packing run as HIP kernels reading the blob in place -- no PCIe
+ * round trip -- and produce the byte-identical image gz_net_set_weights builds on the host.  The
+ * generation roll of a live runner (gz_runner_update_network with device_blob = 1) takes this path. */
 int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_t count);
+/* device milliseconds of the last gz_net_set_weights_device (fold + pack kernels and copies) */
+double gz_net_last_roll_ms(const gz_net* net);
+/* diagnostics: copies the packed device weight image to host memory (out == NULL: returns its size) */
+size_t gz_net_copy_weight_image(gz_net* net, void* out, size_t cap);
 
 /* One contiguous run of boards of a segmented launch.  Pointers may be device memory or pinned host
  * memory (hipHostMalloc): the kernel gathers planes from, and scatters outputs to, each segment
@@ -228,6 +237,8 @@ int gz_runner_update_network(gz_runner* r, const float* blob, size_t count, int 
 /* After a roll: pool_batches[i] = batches of pool i launched on the previous network;
  * *launches_before = launches issued before the swap. */
 int gz_runner_roll_info(gz_runner* r, long* pool_batches, int npools, long* launches_before);
+/* wall milliseconds the launcher spent applying the last roll (the weight fold / pack and swap) */
+double gz_runner_roll_apply_ms(gz_runner* r);
 /* Per-game costs by the game's ordinal within its slot, summed over the runner's pools (struct
  * gz_ordinal_stats, include/gzero_engine.h); a snapshot, safe while the runner runs. */
 struct gz_ordinal_stats;

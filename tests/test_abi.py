@@ -43,3 +43,27 @@ def test_library_loads_and_resolves(header, lib):
     so = ctypes.CDLL(_native.lib_path(lib))
     for name in declared(header):
         assert getattr(so, name) is not None
+
+
+@pytest.mark.parametrize("hw,precision,ok", [((21, 21), "bf16", False), ((19, 19), "fp32", True), ((19, 19), "bf16", True),
+                                              ((13, 13), "fp32", True)])
+def test_net_geometry_check(hw, precision, ok):
+    """gz_net_create checks the board against the compiled kernels before any HIP call (so this runs
+    without a GPU): boards up to 19 x 19 (23 position tiles) are accepted -- the reference's hex19
+    net among them --, larger ones are refused with a clear error instead of failing at launch."""
+    import json
+    from galvanise_zero_amd.nn.desc import NetDesc
+    with open(os.path.join(ROOT, "tests", "golden", "keras_descs.json")) as f:
+        base = json.load(f)["hex19/models/h2_477.json"]["desc"]
+    desc = NetDesc(**dict(base, input_columns=hw[0], input_rows=hw[1]))
+    lib = _native.nn_lib()
+    cdesc = _native.make_net_desc(desc, _native.PRECISIONS[precision])
+    # geometry is checked first; past it gz_net_create needs a device, which this host lacks
+    h = lib.gz_net_create(ctypes.byref(cdesc), 0)
+    err = lib.gz_nn_last_error().decode()
+    if h:
+        lib.gz_net_destroy(h)
+    if ok:
+        assert "unsupported network geometry" not in err, err
+    else:
+        assert not h and "unsupported network geometry F=80 H=21 W=21" in err, err

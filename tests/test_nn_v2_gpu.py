@@ -9,9 +9,12 @@ reference's features=True templates (SE with F // 3 units, templates.py:62-65) o
 random-init weights (the reference's .h5 files are absent).
 
 Tolerances, stated against the float64 oracle, ~3x the worst measured on MI355X over these nets
-(profiles/r02j_v2_gpu_tests.log): bf16 mode max 0.0308 / mean 0.0062 (draughts f1_581, 10 blocks
-behind a 3x3 initial conv); fp32 mode (split operands, boards <= 64 positions) max 1.3e-6 / mean
-2.9e-7 / row KL 1.2e-7.
+(profiles/r05d_nn_gpu_tests.log): bf16 mode max 1.8e-3 / mean 4.1e-4 (hexLG13 b4_305, concat_13x13).
+Until round 5 the bf16 bound was 0.093, set by draughts f1_581 at 0.0308: an im2col swizzle that
+sent chunks past the row for K0 = 160 (a 3x3 initial conv over 15 planes) computed wrong inputs; that
+net now errs 3.4e-4 like the others; fp32 mode (split operands; boards beyond 8 x 8 by the two-pass kernel since
+round 5) 3x the worst over the model files: max 1.73e-6 / mean 6.9e-7 / row KL 4.2e-7 (hexLG13
+b4_305, hex19 h2_477; profiles/r05c_large_board_errors.log).
 """
 import json
 import os
@@ -25,15 +28,15 @@ from oracle import nn_ref
 
 pytestmark = pytest.mark.gpu
 
-TOL_V2_BF16 = (9.3e-2, 1.9e-2)   # max |err|, mean |err|
-TOL_FP32 = (4e-6, 1e-6)
-TOL_FP32_KL = 4e-7               # max over rows of KL(oracle || kernel)
+TOL_V2_BF16 = (5.5e-3, 1.3e-3)   # max |err|, mean |err|: 3x the worst since the im2col fix (r05d: 1.8e-3 / 4.1e-4)
+TOL_FP32 = (5.2e-6, 2.1e-6)
+TOL_FP32_KL = 1.3e-6             # max over rows of KL(oracle || kernel)
 RES_GAMMA = 0.3                  # damps the v2 stream's growth so the softmaxes stay in the interior
 
 with open(os.path.join(os.path.dirname(__file__), "golden", "keras_descs.json")) as _f:
     _ALL = {k: NetDesc(**v["desc"]) for k, v in json.load(_f).items() if "desc" in v and v["desc"]["resnet_v2"]}
-# the kernels hold boards of up to 13 x 13 (176 positions): hex19 (19 x 19, h2_477) is outside them
-FILES = {k: d for k, d in _ALL.items() if d.hw <= 169}
+# every v2 model file, hex19/h2_477 (19 x 19, the 23-tile kernels) included
+FILES = dict(_ALL)
 
 
 def _err(a, b):
@@ -72,8 +75,9 @@ def test_v2_model_files(key, hip_device):
     for n in (1, 19):
         x = random_planes(desc, n, 100 + n)
         _check(key, desc, w, x, hip_device, "bf16", TOL_V2_BF16)
-        if desc.hw <= 64:
-            _check(key, desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
+        # split precision on every board: two boards per workgroup up to 8 x 8, beyond that one board
+        # per workgroup with two passes per conv (P = 2)
+        _check(key, desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
 
 
 GEOM_GAMES = ["breakthroughSmall", "breakthrough", "reversi", "hexLG13", "amazons_10x10"]
@@ -97,8 +101,7 @@ def test_v2_templates(game, hint, hip_device):
     w = random_weights(desc, 7919, bias_std=0.2, res_gamma=RES_GAMMA)
     x = random_planes(desc, 9, 31)
     _check("%s/%s" % (game, hint), desc, w, x, hip_device, "bf16", TOL_V2_BF16)
-    if desc.hw <= 64:
-        _check("%s/%s" % (game, hint), desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
+    _check("%s/%s" % (game, hint), desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
 
 
 V2_NETS = {"b1_58": FILES["breakthroughSmall/models/b1_58.json"], "f2_308": FILES["reversi_8x8/models/f2_308.json"],
@@ -164,8 +167,9 @@ def test_v2_keras_dropin(game, key, hip_device):
 
 
 # concat_all_layers value head (model.py:251-260; the reference's hex19/models/h2_477.json: F = 80,
-# 10 blocks, SE 26, 19 x 19) on synthetic v2 nets the kernels hold: 8 x 8 (two-board kernels, split
-# and bf16) and 13 x 13 (single-image kernel, bf16), with and without squeeze-excite.
+# 10 blocks, SE 26, 19 x 19 -- itself in test_v2_model_files and tests/test_nn_19x19_gpu.py) on
+# synthetic v2 nets: 8 x 8 (two-board kernels) and 13 x 13 (single-image kernels; split by two
+# passes per conv), bf16 and split, with and without squeeze-excite.
 CONCAT_NETS = {
     "concat_8x8_se": NetDesc(5, 8, 8, 128, 6, [155, 155], resnet_v2=True, se_units=42, concat_all_layers=True),
     "concat_8x8_f80": NetDesc(5, 8, 8, 80, 3, [155, 155], value_hidden_size=128, resnet_v2=True, se_units=26,
@@ -185,8 +189,7 @@ def test_v2_concat_all_layers(name, hip_device):
     for n in (1, 300):
         x = random_planes(desc, n, 100 + n)
         _check(name, desc, w, x, hip_device, "bf16", TOL_V2_BF16)
-        if desc.hw <= 64:
-            _check(name, desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
+        _check(name, desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
 
 
 def test_v2_concat_all_layers_batch_invariance(hip_device):

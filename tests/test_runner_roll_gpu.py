@@ -136,6 +136,67 @@ def test_roll_timeout_withdraws_and_next_roll_succeeds(hip_device):
     assert roll["launches_before"] > 0
 
 
+@pytest.mark.timeout(300)
+def test_concurrent_rolls_one_owner(hip_device):
+    """Two callers roll at once: a caller arriving while the other's roll is pending,
+    being applied or not yet collected is rejected ("already pending"); a call that returns 0 had its
+    network applied -- so the net ends on the weights of the last successful call to return."""
+    import threading
+    import time
+    from galvanise_zero_amd._native import HipNet
+    from galvanise_zero_amd.runner import SelfPlayRunner
+    desc = BASELINE_CONFIGS[2]["desc"]
+    setup = Setup("breakthrough")
+    blobs = [to_blob(random_weights(desc, 7921 + i)) for i in range(3)]
+    net = HipNet(desc, hip_device, "fp32")
+    net.set_weights(blobs[0])
+    conf = templates.selfplay_config_template()
+    conf.evals_per_move = 8
+    r = SelfPlayRunner(net, setup.sm, setup.transformer, conf, device=hip_device, num_threads=2, pools_per_thread=2,
+                       batch_size=32, seed=5, spin_yield_playouts=1000, min_launch_rows=64, max_launch_wait_us=2000)
+    r.start()
+    r.wait_rows(128 * 50, timeout_s=120)
+    x = random_planes(desc, 16, 9)
+    refs = []
+    for b in blobs:
+        f = HipNet(desc, hip_device, "fp32")
+        f.set_weights(b)
+        refs.append(f.forward(x))
+    rejected = accepted_both = 0
+    for trial in range(6):
+        res = {}
+        go = threading.Barrier(2)
+
+        def roll(i):
+            go.wait()
+            try:
+                r.update_network(blobs[i], clear_unique_states=False, timeout_s=60)
+                res[i] = ("ok", time.perf_counter())
+            except RuntimeError as e:
+                res[i] = ("err", str(e))
+
+        th = [threading.Thread(target=roll, args=(i,)) for i in (1, 2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        ok = sorted((v[1], i) for i, v in res.items() if v[0] == "ok")
+        errs = [v[1] for v in res.values() if v[0] == "err"]
+        assert ok, res                                  # at least one caller owns the roll
+        for e in errs:
+            assert "already pending" in e, e
+        rejected += len(errs)
+        accepted_both += len(ok) == 2
+        last = ok[-1][1]
+        r.wait_rows(r.stats()["rows"] + 128 * 5, timeout_s=60)
+        got = net.forward(x)
+        for a, b in zip(got, refs[last]):
+            assert np.array_equal(a, b), (trial, res)
+    r.stop()
+    r.close()
+    print("concurrent rolls: %d rejected, %d trials with both applied in turn" % (rejected, accepted_both))
+
+
 @pytest.mark.timeout(400)
 def test_runner_recreate_reuses_node_memory(hip_device):
     """Trees freed by gz_runner_destroy on the caller's thread go back to the process-wide node pool
