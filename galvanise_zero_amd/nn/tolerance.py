@@ -17,8 +17,21 @@ The deep configs' random nets have logits of magnitude 10^2 - 10^4 (no trained .
 softmaxes saturate and a 5e-5 relative logit error moves individual probabilities by up to ~0.05: the
 logits bound is the fp32-class criterion, the probability bounds state what that does to the outputs.
 tests/test_bench_shape_gpu.py, tests/test_nn_gpu.py::test_split_precision_against_fp32 and
-__graft_entry__.smoke() assert these constants.
+__graft_entry__.smoke() assert these constants (test_deep_config_bench_weights asserts each config's
+logits bound on its own, cfg2 included).
+
+The north-star tolerance per config, then:
+  cfg2, cfg3   the probability bounds below (max / mean / KL), on the bench's weights
+  cfg4, cfg5   the relative logits bound below on the bench's (saturating) weights, and in probability
+               space DAMPED_TOLERANCE on damped weights (res_gamma 0.15, interior softmaxes) at the
+               runner's launch shape (>= 1,024 rows in pinned-host segments;
+               tests/test_bench_shape_gpu.py::test_deep_config_damped_at_launch_shape)
 """
+
+# Bounds in probability space for the deep configs on damped weights at the launch shape: 3x the
+# worst measured on MI355X over cfg4 / cfg5 (profiles/r05g_deep_parity.log: max |dp| 4.65e-6, mean
+# 8.1e-7, row KL 1.65e-7) -- fp32-class (tests/test_nn_gpu.py's TOL_FP32 is 2e-4 / 5e-5 / 5e-7)
+DAMPED_TOLERANCE = {"max": 1.4e-5, "mean": 2.5e-6, "kl": 5e-7}
 
 # 3x the max over 10 seeds (measured max in the comment)
 SPLIT_TOLERANCE = {

@@ -25,9 +25,11 @@ from puct_harness import Setup, sample_key
 pytestmark = pytest.mark.gpu
 
 
-def _short_game_conf(evals):
+def _short_game_conf(evals, sample_every_move=False):
     conf = templates.selfplay_config_template()
     conf.evals_per_move = evals
+    if sample_every_move:        # every unique state is sampled (selfplay.cpp:104-118)
+        conf.oscillate_sampling_pct = 1.0
     conf.run_to_end_evals = 4
     conf.resign0_score_probability = conf.resign1_score_probability = 0.95
     conf.resign0_pct = conf.resign1_pct = 0.0
@@ -43,16 +45,20 @@ def _suffix(s):
     return s
 
 
-CASES = {"hexLG13_cfg4": (4, "hexLG13", 16, 250), "amazons_cfg5": (5, "amazons_10x10", 8, 160)}
+# case: (config, game, batch, polls, evals per move, every move sampled, samples required)
+# amazons_cfg5_deep: >= 32 evaluations per sampled move, so the selection over amazons'
+# ~2,000-child roots runs many playouts per move on the GPU forward, and >= 50 compared samples
+CASES = {"hexLG13_cfg4": (4, "hexLG13", 16, 250, 6, False, 4), "amazons_cfg5": (5, "amazons_10x10", 8, 160, 6, False, 4),
+         "amazons_cfg5_deep": (5, "amazons_10x10", 8, 900, 32, True, 50)}
 
 
-@pytest.mark.timeout(900)
+@pytest.mark.timeout(1200)
 @pytest.mark.parametrize("case", list(CASES))
 def test_deep_config_runner_matches_oracle(case, hip_device):
     from galvanise_zero_amd._native import HipNet
     from galvanise_zero_amd.runner import SelfPlayRunner
     from oracle import puct_ref as P
-    cfg, game, B, polls = CASES[case]
+    cfg, game, B, polls, evals, every_move, need = CASES[case]
     desc = BASELINE_CONFIGS[cfg]["desc"]
     setup = Setup(game)
     t = setup.transformer
@@ -60,7 +66,7 @@ def test_deep_config_runner_matches_oracle(case, hip_device):
         (desc.input_channels, desc.input_columns, desc.input_rows, list(desc.policy_dist_count))
     net = HipNet(desc, hip_device, "fp32")          # bench.py's arithmetic: bf16x3 split
     net.set_weights(to_blob(random_weights(desc, 7921)))
-    conf = _short_game_conf(6)
+    conf = _short_game_conf(evals, every_move)
     seed, threads, ppt, spin = 20251019, 2, 2, 1000
     r = SelfPlayRunner(net, setup.sm, t, conf, device=hip_device, num_threads=threads, pools_per_thread=ppt,
                        batch_size=B, seed=seed, keep_samples=True, spin_yield_playouts=spin,
@@ -102,6 +108,6 @@ def test_deep_config_runner_matches_oracle(case, hip_device):
         exp = [sample_key(setup, _suffix(s), False) for s in man.samples[:n]]
         assert got == exp, pool
         checked += n
-    print("%s: %d samples of 2 pools identical to the oracle (%d-block x %d net)" % (
-        case, checked, desc.residual_layers, desc.cnn_filter_size))
-    assert checked >= 4
+    print("%s: %d samples of 2 pools identical to the oracle (%d-block x %d net, %d evals per move)" % (
+        case, checked, desc.residual_layers, desc.cnn_filter_size, evals))
+    assert checked >= need
