@@ -200,7 +200,8 @@ def cpu_model():
 
 
 def cpu_baseline(seconds, evals, mode, batch, config=2):
-    """The reference's CPU self-play design timed on this host: cppinterface.Supervisor with C++
+    """CPU restatement of the reference's CPU self-play design, timed on this host (the
+    reference's own C++ cannot build here -- ggplib / k273 absent): cppinterface.Supervisor with C++
     worker threads (2 pools of `batch` games each, supervisor.cpp:79-99,196-245) running the tree
     search while the Python poll loop (cppinterface.py:131-144) runs the network on the CPU
     (float32 torch, all the rank's cores: oracle/nn_torch.py) -- the same engine and workload as the
@@ -239,9 +240,11 @@ def cpu_baseline(seconds, evals, mode, batch, config=2):
     return {"value": rows / el, "unit": "leaf-evals/s", "cores": cores, "kind": "port",
             "cpu_model": cpu_model(), "worker_threads": workers, "torch_threads": cores,
             "phase": "opening: %.0f-%.0f s after the start of self-play" % (t0 - t_start, t0 - t_start + el),
-            "sample": "%.1f s of %s self-play from the initial position (%d evals/move, %s mode): the reference's "
-                      "worker-thread design (%d C++ worker threads x 2 pools x %d games, Supervisor.poll loop) with "
-                      "a float32 torch-CPU network on %d threads" % (el, sm.game, evals, mode, workers, batch, cores)}
+            "label": "CPU restatement (not the reference's own binary: SURVEY 8c)",
+            "sample": "%.1f s of %s self-play from the initial position (%d evals/move, %s mode): CPU restatement "
+                      "of the reference's worker-thread design (%d C++ worker threads x 2 pools x %d games, "
+                      "Supervisor.poll loop) with a float32 torch-CPU network on %d threads"
+                      % (el, sm.game, evals, mode, workers, batch, cores)}
 
 
 def launch_ranks(args):

@@ -536,6 +536,8 @@ namespace {
 struct SelectScratch {
     std::vector<double> base, expl, inflight, scores;
     std::vector<uint32_t> trav;
+    std::vector<float> pcp;          // puct_constant * policy_prob (float, as the reference's product)
+    std::vector<int32_t> tr1;        // traversals + 1 (the exploration term's int)
     std::vector<uint8_t> kind, bcs;
     std::vector<float> key_s, key_p;
     // sortedChildrenSelect permutation cache, keyed by the sort's input keys only: std::sort's
@@ -552,7 +554,10 @@ struct SelectScratch {
 
     void reserve(int n) {
         if ((int)base.size() >= n) return;
-        base.resize(n); expl.resize(n); inflight.resize(n); scores.resize(n); trav.resize(n);
+        // (expl / pcp / tr1 / inflight padded to whole 4-lane vectors: explorationTerms)
+        const int n4 = (n + 3) & ~3;
+        base.resize(n); expl.resize(n4); inflight.resize(n4); scores.resize(n); trav.resize(n);
+        pcp.resize(n4); tr1.resize(n4);
         kind.resize(n); bcs.resize(n); key_s.resize(n); key_p.resize(n); perm.resize(n); tmp.resize(n);
         perm2.resize(n); mark.resize(n);
         cached_s.resize(n); cached_p.resize(n);
@@ -578,6 +583,26 @@ struct SelectScratch {
 // child kinds of the selection pass
 enum : uint8_t { kSkip = 0, kPrior = 1, kScored = 2, kWinReturn = 3, kBad = 4 };
 }  // namespace
+
+// expl[i] = (double)pcp[i] * sqrt_node_visits / ((double)tr1[i] + inflight[i]) for every child, four
+// at a time (one packed division per four children instead of four scalar ones: the selection pass
+// was bound by the divider), tr1[i] == 0 marking a zero term (a finalised child that is neither a win
+// nor a loss).  The reference's expression `puct_constant * policy_prob * sqrt_node_visits /
+// (traversals + inflight_visits)` is float * float (rounded to float), then * double, then / (int +
+// double): exactly these IEEE operations per lane.  (Padded lanes compute garbage nobody reads.)
+static inline void explorationTerms(const float* pcp, const int32_t* tr1, const double* inflight, double sq,
+                                    double* expl, int n) {
+    const __m256d sq4 = _mm256_set1_pd(sq);
+    const __m256d zero = _mm256_setzero_pd();
+    for (int i = 0; i < n; i += 4) {
+        const __m128i t = _mm_loadu_si128((const __m128i*)(tr1 + i));
+        const __m256d num = _mm256_mul_pd(_mm256_cvtps_pd(_mm_loadu_ps(pcp + i)), sq4);
+        const __m256d den = _mm256_add_pd(_mm256_cvtepi32_pd(t), _mm256_loadu_pd(inflight + i));
+        const __m256d q = _mm256_div_pd(num, den);
+        const __m256d z = _mm256_castsi256_pd(_mm256_cvtepi32_epi64(_mm_cmpeq_epi32(t, _mm_setzero_si128())));
+        _mm256_storeu_pd(expl + i, _mm256_blendv_pd(q, zero, z));
+    }
+}
 
 // The literal selection loop of the reference over sortedChildrenSelect (evaluator.cpp:341-517),
 // kept verbatim for the verification mode (GZ_VERIFY_FASTPATH=1) and for nodes with > 65535
@@ -757,14 +782,17 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
         S.key_p[i] = c->policy_prob_orig;
 
         S.kind[i] = kSkip;
+        // the exploration term's factors; the term itself, node->puct_constant * policy_prob *
+        // sqrt_node_visits / (traversals + 1 + inflight), for every child at once after the pass
+        // (explorationTerms: packed divisions, the same IEEE operations in the same order)
+        const double inflight_visits = cn != nullptr ? cn_inflight : 0;
+        S.pcp[i] = node->puct_constant * c->policy_prob;
+        S.tr1[i] = (int32_t)(c->traversals + 1);
+        S.inflight[i] = inflight_visits;
         if (c->unselectable) continue;
         if (cn != nullptr && (cn_flags & kMirrorAllUnselectable)) continue;
-        const int traversals = c->traversals + 1;
-        const double inflight_visits = cn != nullptr ? cn_inflight : 0;
-        double exploration_score = node->puct_constant * c->policy_prob * sqrt_node_visits /
-                                   (traversals + inflight_visits);
+        bool zero_expl = false;
         S.trav[i] = c->traversals;
-        S.inflight[i] = inflight_visits;
         if (c->traversals > 0 && inflight_visits > 0) rng_steps = true;   // discount draws RNG
         if (cn != nullptr) {
             double child_score = cn_score;
@@ -788,7 +816,7 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
                     S.kind[i] = kBad;   // bad_fallback candidate
                     continue;
                 } else {
-                    exploration_score = 0.0;
+                    zero_expl = true;
                 }
             }
             S.kind[i] = kScored;
@@ -797,13 +825,15 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
         } else {
             S.kind[i] = kPrior;
         }
-        S.expl[i] = exploration_score;
+        if (zero_expl) S.tr1[i] = 0;   // a finalised non-win child: exploration 0 (marked, set below)
         ++reach;
         if (latch && c->traversals > 16 && c->traversals > node->visits * limit_latch_root) {
             ++latch_count;
             latch_d = i;
         }
     }
+
+    explorationTerms(S.pcp.data(), S.tr1.data(), S.inflight.data(), sqrt_node_visits, S.expl.data(), n);
 
     // priorScore (evaluator.cpp:1195-1224)
     float prior_score = node->getFinalScore(lead);
@@ -1971,6 +2001,184 @@ __attribute__((noinline, target("avx2"))) void spin_wins_v(SpinRegs& x, int limi
     x.failed = failed;
 }
 
+// spin_wins_v in blocks of up to 8 playouts (GZ_SPIN_VEC=2).  Everything a playout computes that
+// does not depend on which candidate the earlier playouts chose is computed for the whole block
+// with packed instructions before the block's selections run: the puct constants (table lookups),
+// sqrt(visits + 1) (two packed square roots instead of eight), and the root's current scores -- deep
+// in a spin cur = (v cur + s) / (v + 1) rounds back to cur, so one packed division per role checks
+// eight playouts' updates at once; the block ends at the first playout whose update changes a bit
+// (taken there, exactly as the per-playout loop takes it), at the next root normalisation and at the
+// run's limits.  With cur fixed over the block, the noise check and the policy decay's parameters are
+// the block's too.  What stays per playout is the choice itself: one packed float multiply, one
+// packed double multiply and one packed double division for the NC candidates, and the float-rounded
+// comparisons in candidate order.  Every value is the scalar loop's (IEEE packed arithmetic, no
+// contraction): the choice and the state are the same bit for bit.
+template <int NC>
+__attribute__((noinline, target("avx2"))) void spin_wins_b(SpinRegs& x, int limit) {
+    static_assert(NC >= 2 && NC <= 4, "lanes");
+    constexpr int kB = 8;
+    alignas(32) float Pa[4] = {0.f, 0.f, 0.f, 0.f};
+    alignas(16) int32_t Ta[4] = {0, 0, 0, 0};
+    for (int k = 0; k < NC; ++k) { Pa[k] = x.P[k]; Ta[k] = (int32_t)x.T[k]; }
+    uint32_t LV[NC], T0[NC];
+    for (int k = 0; k < NC; ++k) { LV[k] = x.LV[k]; T0[k] = x.T[k]; }
+    __m128 Pv = _mm_load_ps(Pa);
+    __m128i Tv = _mm_load_si128((const __m128i*)Ta);
+    const __m128i lane_id = _mm_set_epi32(3, 2, 1, 0);
+    const __m128i one_i = _mm_set1_epi32(1);
+    const float win_base = x.BASE[0];
+    const float sc0 = x.lsc[0][0], sc1 = x.lsc[0][1];
+    float cur0 = x.cur[0], cur1 = x.cur[1];
+    const int lead = x.lead;
+    const float limit_latch_root = 0.66;
+    const float pc_root = x.pc_root;
+    const bool noise_check = x.noise_check;
+    const double ub = x.ub;
+    const uint32_t v_end = x.v_end;
+    const uint64_t reach = x.reach;
+    uint32_t v = x.v, touched = 0;
+    float pc = x.pc;
+    uint64_t discards = 0;
+    int done = 0;
+    bool failed = false;
+    PuctLogCursor plog;
+    uint32_t tmax = 0;
+    for (int k = 0; k < NC; ++k) tmax = std::max(tmax, x.T[k]);
+    const uint32_t run_max = std::min<uint32_t>((uint32_t)std::max(limit, 0), v_end - v);
+    const bool check_latch = !((double)tmax + run_max < 0.66 * (double)v * (1.0 - 1e-5));
+    alignas(32) double sa[4];
+    alignas(32) float pcs[kB];
+    alignas(32) double sqs[kB];
+    alignas(32) float n0s[kB], n1s[kB];
+    const __m256i jv = _mm256_set_epi32(7, 6, 5, 4, 3, 2, 1, 0);
+    while (done < limit && v < v_end) {
+        if (noise_check && (lead == 0 ? cur0 : cur1) <= 0.95) {
+            failed = true;
+            break;
+        }
+        // block length: the run's limits and the next root normalisation (after the playout that
+        // brings v to a multiple of 100)
+        int L = kB;
+        L = std::min<int>(L, limit - done);
+        L = std::min<int>(L, (int)(v_end - v));
+        L = std::min<int>(L, 100 - (int)(v % 100));
+        // the block's puct constants and square roots (independent of the choices)
+        for (int j = 0; j < L; ++j) {
+            float p = plog.at(v + j);
+            p += pc_root;
+            pcs[j] = p;
+        }
+        {
+            const __m256i vj1 = _mm256_add_epi32(_mm256_set1_epi32((int)v + 1), jv);   // v + j + 1 (< 2^31)
+            _mm256_store_pd(sqs, _mm256_sqrt_pd(_mm256_cvtepi32_pd(_mm256_castsi256_si128(vj1))));
+            _mm256_store_pd(sqs + 4, _mm256_sqrt_pd(_mm256_cvtepi32_pd(_mm256_extracti128_si256(vj1, 1))));
+        }
+        // the root's current-score updates of the block's playouts with cur held: visits = v + j
+        // (> 100000: 100000 + 0.1 (visits - 100000)), n = (visits cur + s) / (visits + 1)
+        int jchg = L;   // first playout whose update changes cur (it is taken there)
+        {
+            __m256 vis = _mm256_cvtepi32_ps(_mm256_add_epi32(_mm256_set1_epi32((int)v), jv));
+            const __m256 big = _mm256_set1_ps(100000.f);
+            const __m256 adj = _mm256_add_ps(big, _mm256_mul_ps(_mm256_set1_ps(0.1f), _mm256_sub_ps(vis, big)));
+            vis = _mm256_blendv_ps(vis, adj, _mm256_cmp_ps(vis, big, _CMP_GT_OQ));
+            const __m256 den = _mm256_add_ps(vis, _mm256_set1_ps(1.0f));
+            const __m256 n0 = _mm256_div_ps(_mm256_add_ps(_mm256_mul_ps(vis, _mm256_set1_ps(cur0)), _mm256_set1_ps(sc0)), den);
+            const __m256 n1 = _mm256_div_ps(_mm256_add_ps(_mm256_mul_ps(vis, _mm256_set1_ps(cur1)), _mm256_set1_ps(sc1)), den);
+            // bitwise comparison (as the per-playout loop's)
+            const __m256i c0 = _mm256_cmpeq_epi32(_mm256_castps_si256(n0), _mm256_set1_epi32(__builtin_bit_cast(int32_t, cur0)));
+            const __m256i c1 = _mm256_cmpeq_epi32(_mm256_castps_si256(n1), _mm256_set1_epi32(__builtin_bit_cast(int32_t, cur1)));
+            const uint32_t diff = ~(uint32_t)_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_and_si256(c0, c1))) & ((1u << L) - 1);
+            if (diff) {
+                jchg = __builtin_ctz(diff);
+                _mm256_store_ps(n0s, n0);
+                _mm256_store_ps(n1s, n1);
+            }
+        }
+        const int Lb = jchg < L ? jchg + 1 : L;
+        // the policy decay's parameters with cur held (and, for the last playout, with its update)
+        float apply = 1.0f, minimum = 0.0f;
+        decay_params(lead == 0 ? cur0 : cur1, &apply, &minimum);
+        for (int j = 0; j < Lb; ++j) {
+            const uint32_t vj = v + j;
+            pc = pcs[j];
+            const bool latch = vj > 1000 && vj < 40000000;
+            if (check_latch) {
+                _mm_store_si128((__m128i*)Ta, Tv);
+                bool latched_win = false;
+                for (int k = 0; k < NC; ++k) {
+                    const uint32_t t = (uint32_t)Ta[k];
+                    latched_win |= t > 16 && t > vj * limit_latch_root;
+                }
+                if (latch && latched_win) {
+                    failed = true;
+                    break;
+                }
+            }
+            double child_score = win_base;
+            child_score *= 1.0f + pc;
+            const __m128 pcP = _mm_mul_ps(_mm_set1_ps(pc), Pv);
+            const __m256d num = _mm256_mul_pd(_mm256_cvtps_pd(pcP), _mm256_set1_pd(sqs[j]));
+            const __m256d den = _mm256_add_pd(_mm256_cvtepi32_pd(_mm_add_epi32(Tv, one_i)), _mm256_setzero_pd());
+            const __m256d score = _mm256_add_pd(_mm256_set1_pd(child_score), _mm256_div_pd(num, den));
+            _mm256_store_pd(sa, score);
+            float best_score = -1;
+            int best = -1;
+            double best_exact = 0.0;
+            for (int k = 0; k < NC; ++k) {
+                if (sa[k] > best_score) {
+                    best = k;
+                    best_score = sa[k];
+                    best_exact = sa[k];
+                }
+            }
+            if (best < 0 || !(ub < best_exact) || !(ub <= (double)(float)best_exact)) {
+                failed = true;
+                break;
+            }
+            discards += latch ? reach : 0;
+            touched |= 1u << best;
+            if (j == jchg) {   // this playout's update changes cur: taken, and its decay reads it
+                cur0 = n0s[j];
+                cur1 = n1s[j];
+                decay_params(lead == 0 ? cur0 : cur1, &apply, &minimum);
+            }
+            const __m128i sel = _mm_cmpeq_epi32(lane_id, _mm_set1_epi32(best));
+            Tv = _mm_sub_epi32(Tv, sel);
+            if (vj + 1 > 23) {
+                const __m128 mn = _mm_set1_ps(minimum);
+                const __m128 pn = _mm_mul_ps(Pv, _mm_set1_ps(apply));
+                const __m128 clamped = _mm_blendv_ps(mn, pn, _mm_cmplt_ps(mn, pn));
+                const __m128 upd = _mm_and_ps(_mm_castsi128_ps(sel), _mm_cmpgt_ps(Pv, mn));
+                Pv = _mm_blendv_ps(Pv, clamped, upd);
+            }
+            ++done;
+        }
+        v = x.v + done;   // (x.v: the run's first visit count)
+        if (failed) break;
+        if (v % 100 == 0) {
+            _mm_store_ps(Pa, Pv);
+            spin_normalise(x, Pa, NC);
+            Pv = _mm_load_ps(Pa);
+            if (x.expired) break;
+        }
+    }
+    _mm_store_ps(Pa, Pv);
+    _mm_store_si128((__m128i*)Ta, Tv);
+    for (int k = 0; k < NC; ++k) {
+        x.P[k] = Pa[k];
+        x.T[k] = (uint32_t)Ta[k];
+        x.LV[k] = LV[k] + ((uint32_t)Ta[k] - T0[k]);   // the win's visits rise with its traversals
+    }
+    x.cur[0] = cur0;
+    x.cur[1] = cur1;
+    x.v = v;
+    x.pc = pc;
+    x.discards += discards;
+    x.touched |= touched;
+    x.done += done;
+    x.failed = failed;
+}
+
 // any candidate mix (wins and watched scored children)
 void spin_mixed(SpinRegs& x, int limit) {
     const float limit_latch_root = 0.66;
@@ -2079,12 +2287,20 @@ int PuctEvaluator::spinRunRegs(int limit) {
     x.node = node;
     x.cand = spin.cand;
     x.drift = spin.drift;
-    // GZ_SPIN_VEC=1: the AVX2 register loops (A/B; both compute the same playouts)
-    static const bool vec = [] {
+    // Register loops for all-win epochs: GZ_SPIN_VEC=2 (default) the AVX2 loop in blocks of eight
+    // playouts, =1 the AVX2 loop per playout, =0 the scalar loop (all compute the same playouts).
+    // On the GPU box's EPYC 9575F the AVX2 loops ran +4.7 % leaf-evals/s over the scalar one in the
+    // bench's aged window (profiles/r05h_bench_*.log), the block form even with the per-playout one
+    // (profiles/r05i_*; run-to-run spread ~4 %); it does a third of the divider work per playout.
+    static const int vec = [] {
         const char* e = std::getenv("GZ_SPIN_VEC");
-        return e != nullptr && e[0] == '1';
+        return e != nullptr ? std::atoi(e) : 2;
     }();
-    if (all_win && x.role_count == 2 && nc == 2) vec ? spin_wins_v<2>(x, limit) : spin_wins<2, 2>(x, limit);
+    if (all_win && x.role_count == 2 && nc >= 2 && nc <= 4 && vec == 2) {
+        if (nc == 2) spin_wins_b<2>(x, limit);
+        else if (nc == 3) spin_wins_b<3>(x, limit);
+        else spin_wins_b<4>(x, limit);
+    } else if (all_win && x.role_count == 2 && nc == 2) vec ? spin_wins_v<2>(x, limit) : spin_wins<2, 2>(x, limit);
     else if (all_win && x.role_count == 2 && nc == 3) vec ? spin_wins_v<3>(x, limit) : spin_wins<3, 2>(x, limit);
     else if (all_win && x.role_count == 2 && nc == 4) vec ? spin_wins_v<4>(x, limit) : spin_wins<4, 2>(x, limit);
     else spin_mixed(x, limit);

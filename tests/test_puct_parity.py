@@ -194,11 +194,13 @@ def test_spin_fast_path_identical():
     script = os.path.join(os.path.dirname(__file__), "native", "spin_check.py")
     outs = []
     # GZ_SPIN_FAST=2: the fast path without the register-resident runs (evaluator.cpp spinRunRegs)
-    # GZ_SPIN_VEC=1: the AVX2 register loops instead of the scalar ones (evaluator.cpp spin_wins_v)
-    # (the five runs are independent processes: run side by side)
+    # GZ_SPIN_VEC: 2 (default) the AVX2 register loops in blocks of eight playouts (evaluator.cpp
+    # spin_wins_b), 1 the AVX2 loops per playout (spin_wins_v), 0 the scalar ones (spin_wins)
+    # (the six runs are independent processes: run side by side)
     procs = []
     for env in ({"GZ_SPIN_FAST": "0"}, {"GZ_SPIN_FAST": "1"}, {"GZ_SPIN_FAST": "2"},
-                {"GZ_SPIN_FAST": "1", "GZ_VERIFY_FASTPATH": "1"}, {"GZ_SPIN_FAST": "1", "GZ_SPIN_VEC": "1"}):
+                {"GZ_SPIN_FAST": "1", "GZ_VERIFY_FASTPATH": "1"}, {"GZ_SPIN_FAST": "1", "GZ_SPIN_VEC": "1"},
+                {"GZ_SPIN_FAST": "1", "GZ_SPIN_VEC": "0"}):
         e = dict(os.environ, **env)
         procs.append(subprocess.Popen([sys.executable, script, "breakthrough", "16", "3000", "100"], env=e,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
@@ -206,7 +208,7 @@ def test_spin_fast_path_identical():
         out, err = pr.communicate(timeout=600)
         assert pr.returncode == 0, err[-2000:]
         outs.append(json.loads(out.strip().splitlines()[-1]))
-    assert outs[0] == outs[1] == outs[2] == outs[3] == outs[4]
+    assert all(o == outs[0] for o in outs[1:])
     assert outs[0]["samples"] > 50 and outs[0]["tree_playouts"] > 3 * outs[0]["evaluations"]
 
 

@@ -39,7 +39,7 @@ def test_runner_aged_fastpaths_verified(hip_device):
     assert st["window_games_completed"] > 0, st
 
 
-# NN-free (spin) playouts per leaf in the verified window; the bench's window runs at ~414 unverified
-# (BENCH_r03.json).  Verification re-makes every spin playout's selection the literal way, which slows
+# NN-free (spin) playouts per leaf in the verified window; the bench's window runs at ~415 unverified
+# (the driver's BENCH_r04.json; 320-330 in round 5's shorter-aged A/B runs, profiles/r05h_*).  Verification re-makes every spin playout's selection the literal way, which slows
 # spinning games more than evaluating ones, so the window's ratio is measured below the bench's.
 WINDOW_NN_FREE_MIN = 300

@@ -1,0 +1,314 @@
+// MFMA shape probe for the split (bf16x3) residual conv: the headline trunk's
+// inner loop -- per k-step of 32 input channels, B fragments (hi + lo) read from an LDS image with
+// ds_read_b128, A fragments (weights, hi + lo) in registers, each (co tile, position tile) product as
+// a three-MFMA accumulate chain hi*hi + hi*lo + lo*hi -- in the two gfx950 bf16 shapes:
+//   s16: v_mfma_f32_16x16x32_bf16 (the kernel's): per wave 2 co tiles x 8 position tiles of 16,
+//        48 MFMAs + 16 ds_read_b128 per k-step
+//   s32: v_mfma_f32_32x32x16_bf16: per wave 1 co tile of 32 x 4 position tiles of 32, two k halves,
+//        24 MFMAs (twice the FLOPs each) + 16 ds_read_b128 per k-step
+//   s17 / s18: s16 with the B fragments read one k-step ahead into a second register set (the
+//        kernel's unrolled conv), s18 pinning each tile's two reads right after its chains
+//   s22 / s20 / s21: s17 with the weights streamed from a 7 MB device image (the kernel's cfg2 split
+//        trunk weights) through a register ring 2 / 4 / 8 k-steps deep
+// Same FLOPs, same LDS bytes, same accumulator registers (64), one workgroup of 4 waves per CU (the
+// LDS allocation), every CU busy, random data (the clock the chip holds depends on it:
+// MI355X_MICROARCH.md DVFS item 7).  Reports wall time, the in-kernel cycles (s_memtime) and the
+// algorithmic rate (1 of the 3 MFMAs' FLOPs), the split kernel's measure.
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/probes/mfma_shape.hip -o tools/probes/mfma_shape.exe
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+#define CHK(x)                                                                    \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));          \
+            std::exit(1);                                                         \
+        }                                                                         \
+    } while (0)
+
+constexpr int kRowBytes = 544;   // the kernel's padded split rows (hi 256 B | lo 256 B | 32 B pad)
+constexpr int kRows = 128;       // two boards of 64 positions
+constexpr int kLds = 140 * 1024; // one workgroup per CU
+
+__device__ __forceinline__ void chain16(f32x4& acc, const bf16x8& wh, const bf16x8& bh, const bf16x8& bl,
+                                        const bf16x8& wl) {
+    asm volatile(
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %4, %2, %0"
+        : "+a"(acc)
+        : "v"(wh), "v"(bh), "v"(bl), "v"(wl));
+}
+__device__ __forceinline__ void chain32(f32x16& acc, const bf16x8& wh, const bf16x8& bh, const bf16x8& bl,
+                                        const bf16x8& wl) {
+    asm volatile(
+        "v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %0, %1, %3, %0\n\t"
+        "v_mfma_f32_32x32x16_bf16 %0, %4, %2, %0"
+        : "+a"(acc)
+        : "v"(wh), "v"(bh), "v"(bl), "v"(wl));
+}
+
+// SHAPE 16: lane (li = lane % 16, g = lane / 16) reads position tile t's row 16 t + li, chunk g of
+// the k-step (8 channels); SHAPE 32: lane (li = lane % 32, h = lane / 32) reads row 32 t + li, chunk
+// 2 kh + h.  Weight fragments rotate through 4 k-steps' registers (loaded once).
+template <int SHAPE>
+__global__ void __launch_bounds__(256) probe(const bf16x8* __restrict__ wsrc, float* out, unsigned long long* cyc,
+                                             int ksteps) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // random image (a hash of the byte offset; bf16 values of moderate magnitude)
+    for (int i = tid; i < kRows * kRowBytes / 4; i += 256) {
+        unsigned x = (unsigned)(i * 2654435761u) ^ (blockIdx.x * 40503u);
+        x ^= x >> 13;
+        x *= 0x5bd1e995u;
+        x ^= x >> 15;
+        ((unsigned*)lds)[i] = (x & 0x3fff3fffu) | 0x3c003c00u;   // bf16 pairs in [0.0078, 2)
+    }
+    __syncthreads();
+    bf16x8 wh[4][2], wl[4][2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            wh[s][c] = wsrc[((s * 2 + c) * 2 + 0) * 256 + tid];
+            wl[s][c] = wsrc[((s * 2 + c) * 2 + 1) * 256 + tid];
+        }
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    float sum = 0.f;
+    if constexpr (SHAPE == 16) {
+        f32x4 acc[2][8];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(acc[c][t]));
+        asm volatile("s_nop 1" ::: "memory");   // VALU write -> MFMA srcC
+        const int li = lane & 15, g = lane >> 4;
+        for (int k = 0; k < ksteps; k += 4) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int kc = (k + s) & 3;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const char* a = lds + (16 * t + li) * kRowBytes + 16 * (4 * kc + g) % 256;
+                    const bf16x8 bh = *(const bf16x8*)a;
+                    const bf16x8 bl = *(const bf16x8*)(a + 256);
+                    chain16(acc[0][t], wh[s][0], bh, bl, wl[s][0]);
+                    chain16(acc[1][t], wh[s][1], bh, bl, wl[s][1]);
+                }
+            }
+        }
+        asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) sum += acc[c][t][0] + acc[c][t][1] + acc[c][t][2] + acc[c][t][3];
+    } else if constexpr (SHAPE == 17 || SHAPE == 18) {
+        // B fragments one k-step ahead (two register sets), as trunk_kernel's unrolled conv
+        f32x4 acc[2][8];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(acc[c][t]));
+        asm volatile("s_nop 1" ::: "memory");
+        const int li = lane & 15, g = lane >> 4;
+        bf16x8 b[2][8][2];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const char* a = lds + (16 * t + li) * kRowBytes + 16 * g;
+            b[0][t][0] = *(const bf16x8*)a;
+            b[0][t][1] = *(const bf16x8*)(a + 256);
+        }
+        for (int k = 0; k < ksteps; k += 4) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int kn = (k + s + 1) & 3;
+                const int cb = s & 1, nb = cb ^ 1;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    chain16(acc[0][t], wh[s][0], b[cb][t][0], b[cb][t][1], wl[s][0]);
+                    chain16(acc[1][t], wh[s][1], b[cb][t][0], b[cb][t][1], wl[s][1]);
+                    const char* a = lds + (16 * t + li) * kRowBytes + 16 * (4 * kn + g) % 256;
+                    b[nb][t][0] = *(const bf16x8*)a;
+                    b[nb][t][1] = *(const bf16x8*)(a + 256);
+                    if constexpr (SHAPE == 18) {
+                        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the two reads after the chains
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) sum += acc[c][t][0] + acc[c][t][1] + acc[c][t][2] + acc[c][t][3];
+    } else if constexpr (SHAPE >= 20) {
+        // s17 + the weight stream: every k-step's A fragments (hi / lo of 2 co tiles: 4 x 16 B per
+        // lane, 16 KB per workgroup) loaded from a 7 MB image in device memory (the kernel's cfg2
+        // split weights), D = SHAPE - 20 + ... k-steps ahead in a register ring (compiler-tracked loads)
+        constexpr int D = SHAPE == 20 ? 4 : SHAPE == 21 ? 8 : 2;
+        constexpr int NSTEP = 448;   // 7 MB / 16 KB
+        f32x4 acc[2][8];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(acc[c][t]));
+        asm volatile("s_nop 1" ::: "memory");
+        const int li = lane & 15, g = lane >> 4;
+        const bf16x8* wimg = wsrc + 16 * 256 * 8 / 8;   // after the register-weights block
+        auto wl_at = [&](int j, int f) { return wimg[((size_t)(j % NSTEP) * 4 + f) * 256 + tid]; };
+        bf16x8 ring[D][4];
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d)
+#pragma unroll
+            for (int f = 0; f < 4; ++f) ring[d][f] = wl_at(d, f);
+        bf16x8 b[2][8][2];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const char* a = lds + (16 * t + li) * kRowBytes + 16 * g;
+            b[0][t][0] = *(const bf16x8*)a;
+            b[0][t][1] = *(const bf16x8*)(a + 256);
+        }
+        for (int k = 0; k < ksteps; k += D) {
+#pragma unroll
+            for (int s = 0; s < D; ++s) {
+                const int j = k + s;
+#pragma unroll
+                for (int f = 0; f < 4; ++f) ring[(s + D - 1) % D][f] = wl_at(j + D - 1, f);
+                const int kn = (j + 1) & 3;
+                const int cb = s & 1, nb = cb ^ 1;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    chain16(acc[0][t], ring[s][0], b[cb][t][0], b[cb][t][1], ring[s][1]);
+                    chain16(acc[1][t], ring[s][2], b[cb][t][0], b[cb][t][1], ring[s][3]);
+                    const char* a = lds + (16 * t + li) * kRowBytes + 16 * (4 * kn + g) % 256;
+                    b[nb][t][0] = *(const bf16x8*)a;
+                    b[nb][t][1] = *(const bf16x8*)(a + 256);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) sum += acc[c][t][0] + acc[c][t][1] + acc[c][t][2] + acc[c][t][3];
+    } else {
+        f32x16 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) asm volatile("" : "+a"(acc[t]));
+        asm volatile("s_nop 1" ::: "memory");
+        const int li = lane & 31, h = lane >> 5;
+        for (int k = 0; k < ksteps; k += 4) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int kc = (k + s) & 3;
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int kh = 0; kh < 2; ++kh) {
+                        const char* a = lds + (32 * t + li) * kRowBytes + 16 * (4 * kc + 2 * kh + h) % 256;
+                        const bf16x8 bh = *(const bf16x8*)a;
+                        const bf16x8 bl = *(const bf16x8*)(a + 256);
+                        chain32(acc[t], wh[s][kh], bh, bl, wl[s][kh]);
+                    }
+            }
+        }
+        asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sum += acc[t][r];
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[blockIdx.x * 256 + tid] = sum;
+    if (tid == 0) cyc[blockIdx.x] = t1 - t0;
+    (void)wave;
+}
+
+int main(int argc, char** argv) {
+    const int ksteps = argc > 1 ? std::atoi(argv[1]) : 2048;
+    const int grid = argc > 2 ? std::atoi(argv[2]) : 256 * 4;
+    const int reps = argc > 3 ? std::atoi(argv[3]) : 30;
+    // the register weights (16 x 256 fragments), then the 7 MB streamed weight image (448 k-steps x 4 x 256)
+    std::vector<unsigned short> hw((size_t)(16 * 256 + 448 * 4 * 256) * 8);
+    unsigned x = 12345;
+    for (auto& v : hw) {
+        x = x * 1664525u + 1013904223u;
+        v = (unsigned short)(0x3c00 | ((x >> 9) & 0x3ff) | ((x >> 3) & 0x8000));
+    }
+    bf16x8* dw;
+    float* dout;
+    unsigned long long* dcyc;
+    CHK(hipMalloc(&dw, hw.size() * 2));
+    CHK(hipMemcpy(dw, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
+    CHK(hipMalloc(&dout, (size_t)grid * 256 * 4));
+    CHK(hipMalloc(&dcyc, (size_t)grid * 8));
+    CHK(hipFuncSetAttribute((const void*)probe<16>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<32>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<17>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<18>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<20>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<21>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<22>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    hipEvent_t e0, e1;
+    CHK(hipEventCreate(&e0));
+    CHK(hipEventCreate(&e1));
+    // algorithmic FLOPs: per wave per k-step 2 x (32 co x 128 positions x 32 k) (one of the 3 MFMAs)
+    const double flops = (double)grid * 4 * ksteps * 2.0 * 32 * 128 * 32;
+    std::vector<unsigned long long> cyc(grid);
+    for (int round = 0; round < 3; ++round)
+        for (int shape : {16, 17, 18, 32, 22, 20, 21}) {
+            auto launch = [&]() {
+                if (shape == 16) probe<16><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 17) probe<17><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 18) probe<18><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 20) probe<20><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 21) probe<21><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 22) probe<22><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else probe<32><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+            };
+            for (int i = 0; i < 3; ++i) launch();   // warm (and let the clock settle)
+            CHK(hipEventRecord(e0));
+            for (int i = 0; i < reps; ++i) launch();
+            CHK(hipEventRecord(e1));
+            CHK(hipEventSynchronize(e1));
+            float ms = 0.f;
+            CHK(hipEventElapsedTime(&ms, e0, e1));
+            CHK(hipMemcpy(cyc.data(), dcyc, (size_t)grid * 8, hipMemcpyDeviceToHost));
+            double cavg = 0.0;
+            for (auto c : cyc) cavg += (double)c;
+            cavg /= grid;
+            const double per = ms / reps;
+            std::printf("round %d shape %d: %.3f ms per launch, %.0f cycles per workgroup (%.2f cycles per "
+                        "k-step per wave), algorithmic %.1f TFLOP/s (MFMA issued %.1f TFLOP/s)\n",
+                        round, shape, per, cavg, cavg / ksteps, flops / (per * 1e-3) / 1e12,
+                        3 * flops / (per * 1e-3) / 1e12);
+        }
+    return 0;
+}
