@@ -72,7 +72,7 @@ PMC_PER_LAUNCH = {"gznn::trunk_kernel_w8<128, 4, 3>": {
               "1024-row launches, tools/gpu_pmc_r04.sh): busy cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)"}}
 
 
-def per_game_cost(o, threads, slots, run_s):
+def per_game_cost(o, threads, slots, run_s, rate=None):
     """Per-game cost by the game's ordinal within its slot (gz_ordinal_stats of rank 0's runner, the
     whole run): is a slot's k-th game dearer than its first?  Plus the first-game cohort (ordinal 1:
     one game per slot, every game an independent draw from the initial position with its own RNG
@@ -112,6 +112,17 @@ def per_game_cost(o, threads, slots, run_s):
                   "from_first_game_cohort_leaf_evals_per_s": threads * f * c_e / c_s if f and c_s > 0 else None,
                   "note": "completed games are the cheap part of a heavy-tailed per-game cost (DESIGN.md section 6): "
                           "the first figure overstates the stationary rate"}
+    # games/s by renewal (SURVEY 8d metric 2 where no game completes in the window -- configs 4 / 5):
+    # every poll advances each game of a pool by one evaluation, so each slot completes games at
+    # (rate / slots) / E[evals per game].  The first-game cohort's evaluations so far bound
+    # E[evals per game] from below (an upper bound on games/s), exactly once every first game completed.
+    if rate and slots and c_e > 0:
+        mean_e = c_e / slots
+        cohort["games_per_sec_renewal"] = {
+            "value": rate / mean_e, "evals_per_game": mean_e,
+            "kind": "renewal estimate: every slot's first game completed" if o["inflight_games_ord"][0] == 0
+            else "upper bound: %d of %d first games still in progress (counted at their evaluations so far)"
+                 % (o["inflight_games_ord"][0], slots)}
     return {"by_ordinal": rows, "engine_ms_histogram": hist, "first_game_cohort": cohort,
             "stationary_estimate": stationary,
             "completed_games_evals_per_engine_s": ev / es if es > 0 else None,
@@ -589,7 +600,7 @@ def main():
                 gbps = out["roofline"]["traffic"] / (per_variant[dom]["avg_kernel_ms"] / 1e3) / 1e9
                 out["roofline"].update({"mfma_busy_frac": busy, "hbm_GBps": gbps, "hbm_peak_GBps": PEAK_HBM_GBPS,
                                         "hbm_frac": gbps / PEAK_HBM_GBPS, "pmc_source": pmc["source"]})
-        out["per_game_cost"] = per_game_cost(ordinals, threads, games_per_rank, run_s)
+        out["per_game_cost"] = per_game_cost(ordinals, threads, games_per_rank, run_s, rows / T / world if T > 0 else None)
     runner.close()   # frees the games' trees before the CPU baseline
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
