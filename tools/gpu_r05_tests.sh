@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-5 final tree: the GPU suite in two halves (each under its own limit) and the smoke.
+#   fast: everything but the long runner tests;  long: the aged-window verification, deep-config
+#   runner replays, the roll / recreate runner tests
+set -o pipefail
+TAG=${1:-r05t}; PART=${2:-fast}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+T=$R/gpurun_out/$TAG
+mkdir -p $T
+cd $R
+LONG="tests/test_runner_verify_gpu.py tests/test_runner_deep_gpu.py tests/test_runner_roll_gpu.py"
+if [ "$PART" = fast ]; then
+  DESEL=""; for f in $LONG; do DESEL="$DESEL --ignore=$f"; done
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread $DESEL > $T/gpu_fast.log 2>&1
+  rc=$?
+  grep -E "passed|failed|FAILED|ERROR" $T/gpu_fast.log | tail -8
+  [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $T/smoke.log 2>&1 || { echo "smoke failed"; tail -5 $T/smoke.log; exit 1; }
+  cat $T/smoke.log
+else
+  timeout -k 10 1100 python -u -m pytest $LONG -m gpu -v -s --timeout 900 --timeout-method thread > $T/gpu_long.log 2>&1
+  rc=$?
+  grep -E "passed|failed|FAILED|ERROR|identical|verified" $T/gpu_long.log | tail -12
+  exit $rc
+fi

@@ -9,7 +9,9 @@
 //   s17 / s18: s16 with the B fragments read one k-step ahead into a second register set (the
 //        kernel's unrolled conv), s18 pinning each tile's two reads right after its chains
 //   s22 / s20 / s21: s17 with the weights streamed from a 7 MB device image (the kernel's cfg2 split
-//        trunk weights) through a register ring 2 / 4 / 8 k-steps deep
+//        trunk weights) through a register ring 2 / 4 / 8 k-steps deep, each wave-load 1 KB contiguous
+//   s23: s20 with the trunk kernel's own weight layout (each wave-load 16 rows x 64 B)
+//   s24: s20 with the weights staged through an LDS ring by LDS-DMA (global_load_lds_dwordx4)
 // Same FLOPs, same LDS bytes, same accumulator registers (64), one workgroup of 4 waves per CU (the
 // LDS allocation), every CU busy, random data (the clock the chip holds depends on it:
 // MI355X_MICROARCH.md DVFS item 7).  Reports wall time, the in-kernel cycles (s_memtime) and the
@@ -159,11 +161,11 @@ __global__ void __launch_bounds__(256) probe(const bf16x8* __restrict__ wsrc, fl
         for (int c = 0; c < 2; ++c)
 #pragma unroll
             for (int t = 0; t < 8; ++t) sum += acc[c][t][0] + acc[c][t][1] + acc[c][t][2] + acc[c][t][3];
-    } else if constexpr (SHAPE >= 20) {
+    } else if constexpr (SHAPE >= 20 && SHAPE <= 23) {
         // s17 + the weight stream: every k-step's A fragments (hi / lo of 2 co tiles: 4 x 16 B per
         // lane, 16 KB per workgroup) loaded from a 7 MB image in device memory (the kernel's cfg2
         // split weights), D = SHAPE - 20 + ... k-steps ahead in a register ring (compiler-tracked loads)
-        constexpr int D = SHAPE == 20 ? 4 : SHAPE == 21 ? 8 : 2;
+        constexpr int D = SHAPE == 21 ? 8 : SHAPE == 22 ? 2 : 4;
         constexpr int NSTEP = 448;   // 7 MB / 16 KB
         f32x4 acc[2][8];
 #pragma unroll
@@ -177,7 +179,18 @@ __global__ void __launch_bounds__(256) probe(const bf16x8* __restrict__ wsrc, fl
         asm volatile("s_nop 1" ::: "memory");
         const int li = lane & 15, g = lane >> 4;
         const bf16x8* wimg = wsrc + 16 * 256 * 8 / 8;   // after the register-weights block
-        auto wl_at = [&](int j, int f) { return wimg[((size_t)(j % NSTEP) * 4 + f) * 256 + tid]; };
+        // SHAPE 23: the trunk kernel's packed layout ([k-step][co][hi 32 | lo 32] bf16: ROWB = 128 bytes
+        // per output channel per k-step; lane (li, g) reads row co_base + 16 ct + li at byte 16 g of the
+        // part: each 1 KB wave-load touches 16 rows x 64 B, half of each 128 B line); otherwise the
+        // fragments of a wave-load are 1 KB contiguous in lane order
+        auto wl_at = [&](int j, int f) {
+            if constexpr (SHAPE == 23) {
+                const int ct = f >> 1, part = f & 1, co = (tid >> 6) * 32 + 16 * ct + (tid & 15);
+                const char* b = (const char*)wimg + (size_t)(j % NSTEP) * 128 * 128 + co * 128 + part * 64 + 16 * ((tid & 63) >> 4);
+                return *(const bf16x8*)b;
+            }
+            return wimg[((size_t)(j % NSTEP) * 4 + f) * 256 + tid];
+        };
         bf16x8 ring[D][4];
 #pragma unroll
         for (int d = 0; d < D - 1; ++d)
@@ -210,6 +223,67 @@ __global__ void __launch_bounds__(256) probe(const bf16x8* __restrict__ wsrc, fl
             }
         }
         asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) sum += acc[c][t][0] + acc[c][t][1] + acc[c][t][2] + acc[c][t][3];
+    } else if constexpr (SHAPE == 24) {
+        // s20 with the weights staged through LDS by LDS-DMA (global_load_lds_dwordx4, 1 KB per
+        // wave-instruction, no VGPR returns) into a 4-slot LDS ring of 16 KB per k-step (each wave its
+        // own 4 KB), D - 1 = 3 k-steps ahead; A fragments then read with ds_read_b128 (+4 per k-step)
+        constexpr int D = 4, NSTEP = 448;
+        f32x4 acc[2][8];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) asm volatile("" : "+a"(acc[c][t]));
+        asm volatile("s_nop 1" ::: "memory");
+        const int li = lane & 15, g = lane >> 4;
+        const bf16x8* wimg = wsrc + 16 * 256 * 8 / 8;
+        char* ring = lds + kRows * kRowBytes;   // [D][4 waves][4 fragments][64 lanes] x 16 B
+        auto issue = [&](int j, int slot) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(wimg + ((size_t)(j % NSTEP) * 4 + f) * 256 + tid),
+                    (__attribute__((address_space(3))) void*)(ring + ((slot * 4 + wave) * 4 + f) * 1024), 16, 0, 0);
+        };
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d) issue(d, d);
+        bf16x8 b[2][8][2];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const char* a = lds + (16 * t + li) * kRowBytes + 16 * g;
+            b[0][t][0] = *(const bf16x8*)a;
+            b[0][t][1] = *(const bf16x8*)(a + 256);
+        }
+        for (int k = 0; k < ksteps; k += D) {
+#pragma unroll
+            for (int s = 0; s < D; ++s) {
+                const int j = k + s;
+                issue(j + D - 1, (s + D - 1) % D);
+                asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // this k-step's 4 pieces landed
+                const char* wr = ring + ((s * 4 + wave) * 4) * 1024 + 16 * lane;
+                const bf16x8 a0 = *(const bf16x8*)(wr), a1 = *(const bf16x8*)(wr + 1024);
+                const bf16x8 a2 = *(const bf16x8*)(wr + 2048), a3 = *(const bf16x8*)(wr + 3072);
+                const int kn = (j + 1) & 3;
+                const int cb = s & 1, nb = cb ^ 1;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    chain16(acc[0][t], a0, b[cb][t][0], b[cb][t][1], a1);
+                    chain16(acc[1][t], a2, b[cb][t][0], b[cb][t][1], a3);
+                    const char* a = lds + (16 * t + li) * kRowBytes + 16 * (4 * kn + g) % 256;
+                    b[nb][t][0] = *(const bf16x8*)a;
+                    b[nb][t][1] = *(const bf16x8*)(a + 256);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 7" ::: "memory");
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -276,6 +350,8 @@ int main(int argc, char** argv) {
     CHK(hipFuncSetAttribute((const void*)probe<20>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
     CHK(hipFuncSetAttribute((const void*)probe<21>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
     CHK(hipFuncSetAttribute((const void*)probe<22>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<23>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<24>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
     hipEvent_t e0, e1;
     CHK(hipEventCreate(&e0));
     CHK(hipEventCreate(&e1));
@@ -283,7 +359,7 @@ int main(int argc, char** argv) {
     const double flops = (double)grid * 4 * ksteps * 2.0 * 32 * 128 * 32;
     std::vector<unsigned long long> cyc(grid);
     for (int round = 0; round < 3; ++round)
-        for (int shape : {16, 17, 18, 32, 22, 20, 21}) {
+        for (int shape : {17, 20, 23, 24}) {
             auto launch = [&]() {
                 if (shape == 16) probe<16><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else if (shape == 17) probe<17><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
@@ -291,6 +367,8 @@ int main(int argc, char** argv) {
                 else if (shape == 20) probe<20><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else if (shape == 21) probe<21><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else if (shape == 22) probe<22><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 23) probe<23><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 24) probe<24><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else probe<32><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
             };
             for (int i = 0; i < 3; ++i) launch();   // warm (and let the clock settle)
