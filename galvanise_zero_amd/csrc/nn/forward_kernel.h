@@ -414,16 +414,19 @@ struct Ring {
 };
 
 // Issue stage `gs` of the trunk weight stream (clamped to the last stage) into ring slot SLOT.
-// Fragment (step, ct) of a lane: wres + (step*F + 16ct)*64 bytes + woff, woff = lane's row/slice;
-// the stage base is scalar, ct is the instruction's immediate offset.
+// Fragment (step, ct, part) of a lane: wres + step*F*ROWB + (ct*WP + part)*1 KB + woff, woff = the
+// wave's first 16-channel block + 16 bytes * lane (gz_nn.hip wres_index: each fragment is 1 KB in
+// lane order, so a wave's load is one contiguous 1 KB); the stage base is scalar, the fragment's
+// offset the instruction's immediate.
 // Single-image (F = 256) kernels run at the 512-register limit, where the register allocator
 // copies values between VGPRs and AGPRs freely: an inline-asm load's destination could be copied
 // (or its register reused) before the data lands.  They issue the ring with ordinary loads, which
 // the compiler tracks (it places the waits and never copies an in-flight register).
-// byte offset of weight fragment f (= ct * WP + part) within a k-step, relative to the lane's row
+// byte offset of weight fragment f (= ct * WP + part) within a k-step, relative to the wave's first block
 template <int WP, int ROWB, int FR>
 struct FragOff {
-    static constexpr int value = (FR / WP) * 16 * ROWB + (FR % WP) * 64;
+    static_assert(ROWB == 64 * WP, "16 rows x ROWB bytes = WP fragments of 1 KB");
+    static constexpr int value = FR * 1024;
 };
 template <int F, int PTN, int NB, int P, int WG, int SLOT, int PARTS, int FR>
 __device__ __forceinline__ void ring_issue_f(Ring<F, PTN, NB, P, WG>& ring, int k, uint32_t woff, const char* sb) {
@@ -1007,7 +1010,8 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     }
 
     // prime the weight ring: stages 0 .. R-2 of the trunk stream
-    const uint32_t woff = (uint32_t)((co_base + li) * G::ROWB + 16 * g);   // lane's fragment bytes within a k-step
+    static_assert((F / NWV) % 16 == 0, "a wave's output channels are whole 16-channel weight blocks");
+    const uint32_t woff = (uint32_t)((co_base >> 4) * G::WP * 1024 + 16 * lane);   // lane's fragment bytes within a k-step
     const int gmax = (P == 2 ? 4 : 2) * kp.B * G::NST - 1;   // P = 2: two passes per conv
     Ring<F, PTN, NB, P, WG> ring;
     if (kp.B > 0) ring_prime<F, PTN, NB, P, WG>(ring, kp.wres, woff, gmax, std::make_integer_sequence<int, R - 1>{});

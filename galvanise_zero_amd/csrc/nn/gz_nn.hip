@@ -115,6 +115,17 @@ static inline __host__ __device__ uint16_t f2bf(float f) {
     return (uint16_t)(u >> 16);
 }
 
+// Element offset (within one trunk conv's image) of weight [co][ci] of tap `tap`, hi part; the lo
+// part (split precision) sits 512 elements (1 KB) further.  A k-step (tap, 32 input channels) is
+// FP/16 blocks of 16 output channels; block = P2 fragments of 1 KB, each in MFMA A-fragment lane
+// order (lane = co % 16 + 16 * (k / 8), 8 consecutive k per lane), so one wave-wide 16-byte load
+// reads 1 KB contiguous (forward_kernel.h FragOff).
+static inline __host__ __device__ size_t wres_index(int tap, int co, int ci, int FP, int P2) {
+    const int kc = ci >> 5, k = ci & 31;
+    const size_t blk = ((size_t)(tap * (FP >> 5) + kc) * (FP >> 4) + (co >> 4)) * P2;
+    return (blk * 64 + (co & 15) + 16 * (k >> 3)) * 8 + (k & 7);
+}
+
 static int initial_kernel(const gz_net_desc& d) {
     return d.initial_kernel ? d.initial_kernel : (d.resnet_v2 ? 1 : d.cnn_kernel_size);
 }
@@ -527,8 +538,7 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
             }
         }
     }
-    // trunk conv `conv` [3][3][F][F] * scale[co] -> [tap][kc][co][32] (split precision:
-    // [tap][kc][co][hi 32 | lo 32]), bias[co] -> bres
+    // trunk conv `conv` [3][3][F][F] * scale[co] -> wres_index order, bias[co] -> bres
     auto pack_conv = [&](int conv, const float* w, const std::vector<float>& scale, const std::vector<float>& bias) {
         uint16_t* dst = wres.data() + (size_t)P2 * conv * 9 * FP * FP;
         for (int co = 0; co < F; ++co) {
@@ -536,9 +546,9 @@ extern "C" int gz_net_set_weights(gz_net* net, const float* blob, size_t count) 
             for (int tap = 0; tap < 9; ++tap)
                 for (int ci = 0; ci < F; ++ci) {
                     const float v = w[((size_t)tap * F + ci) * F + co] * scale[co];
-                    const size_t o = ((((size_t)tap * KC + ci / 32) * FP + co) * P2) * 32 + (ci % 32);
+                    const size_t o = wres_index(tap, co, ci, FP, P2);
                     dst[o] = f2bf(v);
-                    if (P2 == 2) dst[o + 32] = lo_of(v);
+                    if (P2 == 2) dst[o + 512] = lo_of(v);
                 }
         }
     };
@@ -828,17 +838,16 @@ __global__ void bn_fold_kernel(const BNJob* jobs, float* fold) {
     }
 }
 
-// one trunk conv [3][3][F][F] * scale[co] -> [tap][kc][co][P2 x 32] bf16 (+ its bias row)
+// one trunk conv [3][3][F][F] * scale[co] -> wres_index order, bf16 (+ its bias row)
 __global__ void pack_conv_kernel(const float* w, const float* scale, const float* bias, uint16_t* dst, float* bres,
                                  int F, int FP, int P2) {
     const size_t n = (size_t)9 * F * F;
-    const int KC = FP / 32;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const int co = (int)(i % F), ci = (int)((i / F) % F), tap = (int)(i / ((size_t)F * F));
         const float v = f_mul(w[i], scale[co]);
-        const size_t o = ((((size_t)tap * KC + ci / 32) * FP + co) * P2) * 32 + (ci % 32);
+        const size_t o = wres_index(tap, co, ci, FP, P2);
         dst[o] = f2bf(v);
-        if (P2 == 2) dst[o + 32] = lo_of_dev(v);
+        if (P2 == 2) dst[o + 512] = lo_of_dev(v);
         if (tap == 0 && ci == 0) bres[co] = bias[co];
     }
 }
