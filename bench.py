@@ -407,7 +407,11 @@ def main():
             opening = {"seconds": el, "rows": st["rows"], "leaf_evals_per_s": st["rows"] / el}
         if st["games_completed"] >= age_target or el >= args.age_seconds:
             break
-        runner.wait_rows(st["rows"] + (1 << 18), timeout_s=600)
+        # 2^18 rows, or what the current rate covers until the time limit (at most 10 s) on slow
+        # few-slot runs, so aging ends near --age-seconds
+        rate = st["rows"] / max(el, 1e-3)
+        chunk = int(min(1 << 18, max(1024, rate * min(10.0, max(args.age_seconds - el, 0.5)))))
+        runner.wait_rows(st["rows"] + chunk, timeout_s=600)
         if int(el) // 10 != int(time.perf_counter() - t_start) // 10:
             heartbeat(runner.stats())
     aged = runner.stats()

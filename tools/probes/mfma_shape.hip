@@ -12,6 +12,8 @@
 //        trunk weights) through a register ring 2 / 4 / 8 k-steps deep, each wave-load 1 KB contiguous
 //   s23: s20 with the trunk kernel's own weight layout (each wave-load 16 rows x 64 B)
 //   s24: s20 with the weights staged through an LDS ring by LDS-DMA (global_load_lds_dwordx4)
+//   s25 / s26: s20 with the waves split 2 x 2 (co half x board): twice the weight loads, half the
+//        B reads per k-step; ring 4 / 2
 // Same FLOPs, same LDS bytes, same accumulator registers (64), one workgroup of 4 waves per CU (the
 // LDS allocation), every CU busy, random data (the clock the chip holds depends on it:
 // MI355X_MICROARCH.md DVFS item 7).  Reports wall time, the in-kernel cycles (s_memtime) and the
@@ -288,6 +290,61 @@ __global__ void __launch_bounds__(256) probe(const bf16x8* __restrict__ wsrc, fl
         for (int c = 0; c < 2; ++c)
 #pragma unroll
             for (int t = 0; t < 8; ++t) sum += acc[c][t][0] + acc[c][t][1] + acc[c][t][2] + acc[c][t][3];
+    } else if constexpr (SHAPE == 25 || SHAPE == 26) {
+        // s20 split 2 x 2 over the workgroup: wave w owns co half (w & 1) (4 co tiles) and board
+        // (w >> 1) (4 position tiles): per k-step 8 weight fragments streamed (twice s20's) and 8
+        // ds_read_b128 of B (half of s20's) for the same 48 MFMAs; ring 4 (s25) / 2 (s26) k-steps
+        constexpr int D = SHAPE == 25 ? 4 : 2, NSTEP = 448;
+        f32x4 acc[4][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) asm volatile("" : "+a"(acc[c][t]));
+        asm volatile("s_nop 1" ::: "memory");
+        const int li = lane & 15, g = lane >> 4, half = wave & 1, board = wave >> 1;
+        const bf16x8* wimg = wsrc + 16 * 256 * 8 / 8;
+        auto wl_at = [&](int j, int f) { return wimg[((size_t)(j % NSTEP) * 16 + half * 8 + f) * 64 + lane]; };
+        bf16x8 ring[D][8];
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d)
+#pragma unroll
+            for (int f = 0; f < 8; ++f) ring[d][f] = wl_at(d, f);
+        bf16x8 b[2][4][2];
+        const char* img = lds + board * 64 * kRowBytes;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const char* a = img + (16 * t + li) * kRowBytes + 16 * g;
+            b[0][t][0] = *(const bf16x8*)a;
+            b[0][t][1] = *(const bf16x8*)(a + 256);
+        }
+        for (int k = 0; k < ksteps; k += D) {
+#pragma unroll
+            for (int s = 0; s < D; ++s) {
+                const int j = k + s;
+#pragma unroll
+                for (int f = 0; f < 8; ++f) ring[(s + D - 1) % D][f] = wl_at(j + D - 1, f);
+                const int kn = (j + 1) & 3;
+                const int cb = s & 1, nb = cb ^ 1;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) chain16(acc[c][t], ring[s][2 * c], b[cb][t][0], b[cb][t][1], ring[s][2 * c + 1]);
+                    const char* a = img + (16 * t + li) * kRowBytes + 16 * (4 * kn + g) % 256;
+                    b[nb][t][0] = *(const bf16x8*)a;
+                    b[nb][t][1] = *(const bf16x8*)(a + 256);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) sum += acc[c][t][0] + acc[c][t][1] + acc[c][t][2] + acc[c][t][3];
     } else {
         f32x16 acc[4];
 #pragma unroll
@@ -352,6 +409,8 @@ int main(int argc, char** argv) {
     CHK(hipFuncSetAttribute((const void*)probe<22>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
     CHK(hipFuncSetAttribute((const void*)probe<23>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
     CHK(hipFuncSetAttribute((const void*)probe<24>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<25>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<26>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
     hipEvent_t e0, e1;
     CHK(hipEventCreate(&e0));
     CHK(hipEventCreate(&e1));
@@ -359,7 +418,7 @@ int main(int argc, char** argv) {
     const double flops = (double)grid * 4 * ksteps * 2.0 * 32 * 128 * 32;
     std::vector<unsigned long long> cyc(grid);
     for (int round = 0; round < 3; ++round)
-        for (int shape : {17, 20, 23, 24}) {
+        for (int shape : {17, 20, 25, 26}) {
             auto launch = [&]() {
                 if (shape == 16) probe<16><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else if (shape == 17) probe<17><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
@@ -369,6 +428,8 @@ int main(int argc, char** argv) {
                 else if (shape == 22) probe<22><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else if (shape == 23) probe<23><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else if (shape == 24) probe<24><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 25) probe<25><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 26) probe<26><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else probe<32><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
             };
             for (int i = 0; i < 3; ++i) launch();   // warm (and let the clock settle)
