@@ -180,7 +180,10 @@ __host__ __device__ constexpr int lcm_c(int a, int b) { return a / gcd_c(a, b) *
 // WG = wave groups per workgroup: 1 (4 waves for NB boards) or 2 (8 waves, 2 per SIMD: group g takes
 // board g of the workgroup with NB = 1; the register budget is then 256 per wave); WG = 3: ONE group
 // of 8 waves for the NB boards, each wave a half of the 4-wave layout's output channels (CT halves:
-// the same weight stream per workgroup, two waves per SIMD, 256 registers per wave)
+// the same weight stream per workgroup, two waves per SIMD, 256 registers per wave); WG = 4: two
+// groups of 2 waves, a board each (NB = 1), each wave half the output channels of its board (twice
+// the 4-wave layout's co tiles, half its position tiles: half the B-fragment reads per MFMA, twice
+// the weight fragments)
 template <int F, int PTN, int NB = 1, int P = 1, int WG = 1>
 struct Geo {
     static constexpr int P2 = P == 3 ? 2 : 1;        // bf16 parts per activation in the LDS image
@@ -189,8 +192,8 @@ struct Geo {
     static constexpr int NPOS = 16 * PTN;            // position capacity (the real count is kp.npos)
     static constexpr int PT = PTN;                   // position tiles per board (MFMA N)
     static constexpr int TT = NB * PT;               // position tiles per wave (all boards)
-    static constexpr int NWV = WG == 3 ? 8 : 4;      // waves per group
-    static constexpr int NGR = WG == 2 ? 2 : 1;      // wave groups per workgroup
+    static constexpr int NWV = WG == 3 ? 8 : WG == 4 ? 2 : 4;   // waves per group
+    static constexpr int NGR = WG == 2 || WG == 4 ? 2 : 1;      // wave groups per workgroup
     static constexpr int CT = F / (16 * NWV);        // co tiles per wave (MFMA M)
     static constexpr int KC = F / 32;                // k-steps per tap
     static constexpr int CPR = F / 8;                // 16-byte chunks of channels per row
@@ -227,8 +230,8 @@ struct Geo {
     static constexpr int NST = 9 * KC / KS;          // ring stages per conv
     // ring depth; the two-board split kernels take exactly one tap's stages (R = KC / KS) so the
     // looped conv's body is one tap (a deeper ring made the body three taps and spilled)
-    static constexpr int R0 = (P2 == 2 && (NB == 2 || WG == 2) && (KC / KS) >= 3 && NST % (KC / KS) == 0 &&
-                               (KC / KS) * KS * NFR * 4 <= 96)
+    static constexpr int R0 = (P2 == 2 && (NB == 2 || WG == 2 || WG == 4) && (KC / KS) >= 3 && NST % (KC / KS) == 0 &&
+                               (KC / KS) * KS * NFR * 4 <= (WG == 4 ? 128 : 96))
                                   ? KC / KS
                                   : ring_depth(NST, KS, NFR, CT >= 4 ? 64 : 96);
     // Single-image mode: when two ping-pong images (+ bias table) do not fit the 160 KB of LDS
@@ -259,10 +262,10 @@ struct Geo {
     // accumulators + residual) the register allocator moves values between VGPRs and AGPRs, and a
     // copy of an inline-asm load's destination could be taken before the data lands; such kernels
     // (and the single-image ones) issue the ring with ordinary loads, which the compiler waits for.
-    static constexpr bool TRACKED = SI || LIVE_VGPRS > 300 || (P2 == 2 && (NB == 2 || WG == 2));
+    static constexpr bool TRACKED = SI || LIVE_VGPRS > 300 || (P2 == 2 && (NB == 2 || WG == 2 || WG == 4));
     static_assert(F % 64 == 0, "filters must be a multiple of 64");
     static_assert(!SI || NB == 1, "single-image mode takes one board per workgroup");
-    static_assert(WG == 1 || (WG == 2 && NB == 1 && !SI) || (WG == 3 && !SI && CT >= 1), "wave groups: two images");
+    static_assert(WG == 1 || ((WG == 2 || WG == 4) && NB == 1 && !SI) || (WG == 3 && !SI && CT >= 1), "wave groups: two images");
     static_assert(!RG || SI, "the global residual is implemented for single-image kernels");
     static constexpr int RESID_BYTES = RG ? 4 * CT * TT * 64 * 16 : 0;   // per workgroup
     // P = 2: the lo image of each workgroup (device scratch after the grid's residual scratch)
@@ -941,7 +944,7 @@ __device__ __forceinline__ void save_lo_write_hi(char* X, char* xlo, const f32x4
 template <int F, int PTN, int NB, int WPE, int P, bool V2, int WG = 1>
 __device__ __forceinline__ void trunk_body(const KParams& kp) {
     using G = Geo<F, PTN, NB, P, WG>;
-    static_assert(P == 1 || (P == 3 && (NB == 1 || G::WRAP) && (G::CT <= 2 || G::SI)) || (P == 2 && G::SI && (!V2 || kLoDirect)),
+    static_assert(P == 1 || (P == 3 && (NB == 1 || G::WRAP) && (G::CT * G::TT <= 16 || G::SI)) || (P == 2 && G::SI && (!V2 || kLoDirect)),
                   "split precision: F <= 128 (F = 256: single image)");
     constexpr int P2 = G::P2;
     constexpr int IP2 = G::WP;    // bf16 parts of the initial conv's operands (im2col scratch, w0 / w0lo)
@@ -969,7 +972,7 @@ __device__ __forceinline__ void trunk_body(const KParams& kp) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // wave group grp (WG = 2: threads 256 grp .. 256 grp + 255) takes boards NB grp .. of the
     // workgroup; LDS: image set 0 [WG][NB][ACT], image set 1 [WG][NB][ACT], bias table
-    const int grp = NGR == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+    const int grp = NGR == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kThreads));
     char* X0 = smem + grp * NB * ACT;                                  // [NB][ACT]
     char* X1 = SI ? smem : smem + NGR * NB * ACT + grp * NB * ACT;      // [NB][ACT]
     char* SCR = X1;                  // scratch aliases X1 while X1 holds no live activations
@@ -1604,6 +1607,15 @@ template <int F, int PTN, int P>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 trunk_kernel_w8(const KParams kp) {
     trunk_body<F, PTN, 2, 2, P, false, 3>(kp);
+}
+
+// Two wave groups of 2 (4 waves, one per SIMD, a board per group; variant 23): each wave multiplies
+// 4 co tiles by its board's position tiles, so a k-step reads half the B fragments of the two-board
+// kernel for the same MFMAs and streams twice the weight fragments
+template <int F, int PTN, int P>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+trunk_kernel_h2(const KParams kp) {
+    trunk_body<F, PTN, 1, 1, P, false, 4>(kp);
 }
 
 template <int F, int PTN, int NB, int WPE, int P>

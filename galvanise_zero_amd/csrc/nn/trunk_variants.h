@@ -65,6 +65,18 @@ KernelChoice kernelw8_for() {
     return k;
 }
 
+// two wave groups of two waves, one board each (variant 23)
+template <int F, int PTN, int P>
+KernelChoice kernelh2_for() {
+    KernelChoice k;
+    k.fn = (const void*)&trunk_kernel_h2<F, PTN, P>;
+    k.act_bytes = Geo<F, PTN, 1, P, 4>::ACT_BYTES;
+    k.nb = 2;
+    k.groups = 2;
+    std::snprintf(k.name, sizeof(k.name), "gznn::trunk_kernel_h2<%d, %d, %d>", F, PTN, P);
+    return k;
+}
+
 // precision 3: split (hi / lo) operands; otherwise bf16.  v = NB * 10 + WPE; 22 = two boards as two
 // groups of four waves (trunk_kernel8).
 template <int F, int PTN, bool V2 = false>
@@ -97,8 +109,10 @@ KernelChoice variants(int v, int precision) {
                     if (v == 21) return kernel_for<F, PTN, 2, 1, 3, V2>();
                     if constexpr (!V2) {
                         if (v == 22) return kernel8_for<F, PTN, 3>();
-                        if constexpr (F == 128)
+                        if constexpr (F == 128) {
                             if (v == 24) return kernelw8_for<F, PTN, 3>();
+                            if (v == 23) return kernelh2_for<F, PTN, 3>();
+                        }
                     }
                 }
             }

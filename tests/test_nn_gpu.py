@@ -246,7 +246,7 @@ def test_template_geometries(game, hint, hip_device):
             assert er[0] <= tol[0] and er[1] <= tol[1], (game, hint, precision, i, er)
 
 
-@pytest.mark.parametrize("variant", ["11", "21", "22", "24"])
+@pytest.mark.parametrize("variant", ["11", "21", "22", "23", "24"])
 def test_kernel_variants_identical_fp32(variant, hip_device, monkeypatch):
     """The split-precision kernels (one or two boards per workgroup; 22: two boards as two groups of
     four waves, trunk_kernel8) compute every row identically (33 rows: a dead board in the last
@@ -266,9 +266,10 @@ def test_kernel_variants_identical_fp32(variant, hip_device, monkeypatch):
 
 
 @pytest.mark.parametrize("n", [512, 1031])
-@pytest.mark.parametrize("variant", ["22", "24"])
+@pytest.mark.parametrize("variant", ["22", "23", "24"])
 def test_wave_group_kernel_identical_at_bench_size(variant, n, hip_device, monkeypatch):
-    """The 8-wave kernels (variant 22, trunk_kernel8: one board per group of four waves; 24,
+    """The wave-group kernels (variant 22, trunk_kernel8: one board per group of four waves; 23,
+    trunk_kernel_h2: one board per group of two waves, each half the board's channels; 24,
     trunk_kernel_w8: one group of eight waves, each half of a 4-wave layout's channels) against the
     two-board kernel (21) at launch sizes of the bench (one and three workgroup rounds): bit-identical."""
     from galvanise_zero_amd._native import HipNet
