@@ -97,9 +97,12 @@ extern "C" const char* gz_nn_last_error(void) { return g_err.c_str(); }
 // large launches: the two-board 4-wave kernel (21).  The 8-wave kernel (24) is 5 % faster back to
 // back (profiles/r04t_w8_kexp.txt) but equal inside the bench, whose launches arrive with gaps
 // (0.4954 vs 0.4942 ms per 1,024-row launch, same box; profiles/r04x_variants_in_bench.txt):
-// selectable (GZ_KERNEL_VARIANT=24), bit-identical.  kLargeFallback: where kLargeVariant is not
-// compiled for a geometry.
-constexpr int kSmallVariant = 11, kLargeVariant = 21, kLargeFallback = 21, kLargeMinRows = 257;
+// selectable (GZ_KERNEL_VARIANT=24), bit-identical.  Round 5: the split F = 128 kernels of boards up
+// to 64 positions take variant 23 (trunk_kernel_h2: two groups of two waves, a board each -- half the
+// B-fragment reads per MFMA), 1-1.5 % faster than 21 at 1,024 rows (profiles/r05t_ab_v23.txt) and
+// bit-identical (the kernels build with -ffp-contract=on).  kLargeFallback: where kLargeVariant is
+// not compiled for a geometry.
+constexpr int kSmallVariant = 11, kLargeVariant = 23, kLargeFallback = 21, kLargeMinRows = 257;
 constexpr int kCUs = 256;
 
 static KernelChoice select_kernel(int fpad, int pt, int v, int precision, bool v2) {

@@ -1,6 +1,6 @@
 """The benched forward at the shapes and weights the bench runs, against the float64 oracle.
 
-bench.py times cfg2's split (bf16x3) large-launch kernel (trunk_kernel<128, 4, 2, 1, 3>, variant 21) inside the runner: launches of
+bench.py times cfg2's split (bf16x3) large-launch kernel (trunk_kernel_h2<128, 4, 3>, variant 23) inside the runner: launches of
 ~1,000 rows = two to three workgroup rounds, composed of several pools' segments (a pool's batch may
 be split between two launches), planes DMA'd into an HBM staging buffer, outputs written straight
 into the pools' pinned host buffers, on the bench's undamped random weights

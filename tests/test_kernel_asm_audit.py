@@ -61,7 +61,8 @@ def test_auditor_rule3_loop_copy():
 
 
 # every trunk instantiation that runs the split looped conv (the F = 128 split kernels, v1 and v2,
-# one and two boards, the two-group and the 8-wave kernels), in one translation unit
+# one and two boards, the two-group, the 8-wave and the two-groups-of-two kernels), in one
+# translation unit (compiled with the library's flags)
 AUDIT_TU = """#include "trunk_variants.h"
 namespace gznn {
 template __global__ void trunk_kernel<128, 2, 1, 1, 3>(KParams);
@@ -76,6 +77,8 @@ template __global__ void trunk_kernel8<128, 4, 3>(KParams);
 template __global__ void trunk_kernel_w8<128, 2, 3>(KParams);
 template __global__ void trunk_kernel_w8<128, 3, 3>(KParams);
 template __global__ void trunk_kernel_w8<128, 4, 3>(KParams);
+template __global__ void trunk_kernel_h2<128, 2, 3>(KParams);
+template __global__ void trunk_kernel_h2<128, 4, 3>(KParams);
 }
 """
 
@@ -86,11 +89,12 @@ def test_compiled_chains_hazard_free(tmp_path):
     src.write_text(AUDIT_TU)
     out = tmp_path / "audit_tu.s"
     subprocess.check_call([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-parameter",
-                           "--cuda-device-only", "-S", "-I", NN, "-o", str(out), str(src)],
+                           "-ffp-contract=on", "--cuda-device-only", "-S", "-I", NN, "-o", str(out), str(src)],
                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     res = kaa.audit(out.read_text())
-    assert len(res) == 12, sorted(res)    # every instantiation above runs chains
+    assert len(res) == 14, sorted(res)    # every instantiation above runs chains
     for name, (n, bad) in res.items():
         assert n > 0
         assert bad == [], (name, bad[:5])
-    assert any("ILi128ELi4ELi2ELi1ELi3E" in k for k in res)   # the headline kernel
+    assert any("ILi128ELi4ELi2ELi1ELi3E" in k for k in res)   # the round-4 headline kernel
+    assert any("trunk_kernel_h2ILi128ELi4ELi3E" in k for k in res)   # the headline kernel
