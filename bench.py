@@ -141,6 +141,8 @@ def parse():
     ap.add_argument("--age-games", type=float, default=3.0,
                     help="steady state: age the game population until this many games per game slot completed ...")
     ap.add_argument("--age-seconds", type=float, default=400.0, help="... or this many seconds passed (0: no aging)")
+    ap.add_argument("--exit-after-line", action="store_true",
+                    help="with --no-cpu-baseline on one GPU: exit right after the line, without stopping the runner")
     ap.add_argument("--threads", type=int, default=0, help="engine threads per GPU (0: the rank's CPU share)")
     ap.add_argument("--pools", type=int, default=2, help="game pools per engine thread")
     ap.add_argument("--batch", type=int, default=256)
@@ -442,7 +444,6 @@ def main():
     ordinals = runner.ordinal_stats()
     run_s = time.perf_counter() - t_start
     barrier()
-    runner.stop()
     elapsed = t1 - t0
 
     d = {k: s1[k] - s0[k] for k in s1}
@@ -605,10 +606,20 @@ def main():
                 out["roofline"].update({"mfma_busy_frac": busy, "hbm_GBps": gbps, "hbm_peak_GBps": PEAK_HBM_GBPS,
                                         "hbm_frac": gbps / PEAK_HBM_GBPS, "pmc_source": pmc["source"]})
         out["per_game_cost"] = per_game_cost(ordinals, threads, games_per_rank, run_s, rows / T / world if T > 0 else None)
+    # The runner is stopped only now: every figure above comes from the snapshots taken at the end
+    # of the timed steps.  A stop waits for each engine thread's current poll, which can sit inside
+    # a long NN-free root spin (minutes on few-slot hexLG13 / amazons runs), so without a CPU leg
+    # the line is printed first.
+    line_first = rank == 0 and (world > 1 or args.no_cpu_baseline)
+    if line_first:
+        print(json.dumps(out), flush=True)
+        if args.exit_after_line:   # few-slot length runs: do not wait out the engine threads' spins
+            sys.stdout.flush()
+            os._exit(0)
+    runner.stop()
     runner.close()   # frees the games' trees before the CPU baseline
-    if rank == 0:
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, evals, args.mode, args.batch, args.config)
+    if rank == 0 and not line_first:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, evals, args.mode, args.batch, args.config)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
