@@ -15,7 +15,7 @@ for c in $CFGS; do
       python3 $R/bench.py --gpus 1 --config $c --steps 10 --warmup 3 --age-seconds $AGE --no-cpu-baseline \
       > $T/bench_cfg$c.log 2>&1 || { echo "cfg$c failed"; tail -5 $T/bench_cfg$c.log; exit 1; }
   find $T/cfg$c -name "*kernel_trace.csv" -delete
-  tail -1 $T/bench_cfg$c.log | cut -c1-300
+  grep "^{" $T/bench_cfg$c.log | tail -1 | cut -c1-300
   find $T/cfg$c -name "*kernel_stats.csv" -exec head -4 {} \; | cut -c1-200
 done
 echo ALL OK

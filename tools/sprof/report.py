@@ -1,11 +1,12 @@
-"""Symbolize tools/sprof samples: python tools/sprof/report.py /tmp/sprof.out [top] [--inline]
-Prints the share of samples per function (the innermost inlined frame with --inline)."""
+"""Symbolize tools/sprof samples: python tools/sprof/report.py /tmp/sprof.out [top] [--inline] [--lines]
+Prints the share of samples per function (the innermost inlined frame with --inline; with --lines
+per outermost function and the innermost frame's source line)."""
 import collections
 import subprocess
 import sys
 
 
-def main(path, top=40, inline=False):
+def main(path, top=40, inline=False, by_line=False):
     maps, samples = [], []
     for line in open(path):
         if line.startswith("M "):
@@ -33,7 +34,13 @@ def main(path, top=40, inline=False):
         out = subprocess.run(args, input="\n".join("%x" % p for p in uniq), capture_output=True, text=True).stdout
         lines = out.splitlines()
         names = {}
-        if inline:
+        if by_line:
+            for p in uniq:
+                r = subprocess.run(["addr2line", "-C", "-f", "-i", "-e", obj, "%x" % p], capture_output=True, text=True)
+                fr = r.stdout.splitlines()
+                # frames innermost first: (function, file:line) pairs
+                names[p] = ("%s | %s" % (fr[-2][:80], fr[1].split("/")[-1])) if len(fr) >= 2 else "?"
+        elif inline:
             # with -i each address prints 2 lines per frame; take the first (innermost) frame
             i = 0
             res = subprocess.run(["addr2line", "-C", "-f", "-i", "-e", obj], input="\n".join("%x" % p for p in uniq),
@@ -57,4 +64,4 @@ def main(path, top=40, inline=False):
 
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    main(args[0], int(args[1]) if len(args) > 1 else 40, "--inline" in sys.argv)
+    main(args[0], int(args[1]) if len(args) > 1 else 40, "--inline" in sys.argv, "--lines" in sys.argv)
