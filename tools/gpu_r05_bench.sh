@@ -7,6 +7,10 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 T=$R/gpurun_out/$TAG
 mkdir -p $T
 cd $R
+# heartbeat under gpurun_out (long tests -- the oracle replays -- print nothing for minutes)
+( while sleep 60; do date +%T >> $T/heartbeat.txt; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 if [ "$PART" = bench ]; then
   timeout -k 10 1000 python -u bench.py > $T/bench.log 2>&1 || { echo "bench failed"; tail -5 $T/bench.log; exit 1; }
   grep "^{" $T/bench.log | tail -1 | cut -c1-400

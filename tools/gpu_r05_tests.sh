@@ -8,6 +8,10 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 T=$R/gpurun_out/$TAG
 mkdir -p $T
 cd $R
+# heartbeat under gpurun_out (long tests -- the oracle replays -- print nothing for minutes)
+( while sleep 60; do date +%T >> $T/heartbeat.txt; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 LONG="tests/test_runner_verify_gpu.py tests/test_runner_deep_gpu.py tests/test_runner_roll_gpu.py"
 if [ "$PART" = fast ]; then
   DESEL=""; for f in $LONG; do DESEL="$DESEL --ignore=$f"; done
