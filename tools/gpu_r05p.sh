@@ -8,7 +8,7 @@ T=$R/gpurun_out/$TAG
 mkdir -p $T
 cd $R
 gcc -O2 -shared -fPIC tools/sprof/sprof.c -o $T/sprof.so || exit 1
-GZ_SPROF_LIB=$T/sprof.so SPROF_OUT=$T/sprof.out SPROF_START_S=330 SPROF_STOP_S=390 timeout -k 10 700 python -u bench.py --gpus 1 --steps 60 --warmup 5 --no-cpu-baseline > $T/bench.log 2>&1 || { echo "bench failed"; tail -20 $T/bench.log; exit 1; }
+GZ_SPROF_LIB=$T/sprof.so SPROF_OUT=$T/sprof.out SPROF_START_S=300 SPROF_STOP_S=335 timeout -k 10 700 python -u bench.py --gpus 1 --steps 60 --warmup 5 --no-cpu-baseline > $T/bench.log 2>&1 || { echo "bench failed"; tail -20 $T/bench.log; exit 1; }
 grep "^{" $T/bench.log | tail -1 | cut -c1-400
 python tools/sprof/report.py $T/sprof.out 60 > $T/sprof_report.txt 2>&1 || exit 1
 python tools/sprof/report.py $T/sprof.out 80 --lines > $T/sprof_lines.txt 2>&1 || exit 1
