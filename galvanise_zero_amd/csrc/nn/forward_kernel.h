@@ -156,7 +156,16 @@ constexpr bool kEpiInConv = false;
 // two ways).  Bit-identical but no faster (profiles/r04za_store_swap_kexp.txt: 0.543-0.547 against
 // 0.547-0.549 ms per 1,024-row launch, residual blocks 79.3 against 78.4 us): the stores are off the
 // critical path, so off; kept for experiments (kexp swapon)
-constexpr bool kStoreSwap = false;
+#ifndef GZ_STORE_SWAP
+#define GZ_STORE_SWAP 0
+#endif
+constexpr bool kStoreSwap = GZ_STORE_SWAP != 0;
+
+// variant 23's weight ring: one tap of stages (128 VGPRs) by default; 96 gives a 2-stage ring
+// (experiments: -DGZ_H2_RING_VGPRS=96)
+#ifndef GZ_H2_RING_VGPRS
+#define GZ_H2_RING_VGPRS 128
+#endif
 
 // ring depth: largest R dividing the stages per conv with R slots of KS*CT fragments <= cap VGPRs
 __host__ __device__ constexpr int ring_depth(int nst, int ks, int ct, int cap) {
@@ -231,7 +240,7 @@ struct Geo {
     // ring depth; the two-board split kernels take exactly one tap's stages (R = KC / KS) so the
     // looped conv's body is one tap (a deeper ring made the body three taps and spilled)
     static constexpr int R0 = (P2 == 2 && (NB == 2 || WG == 2 || WG == 4) && (KC / KS) >= 3 && NST % (KC / KS) == 0 &&
-                               (KC / KS) * KS * NFR * 4 <= (WG == 4 ? 128 : 96))
+                               (KC / KS) * KS * NFR * 4 <= (WG == 4 ? GZ_H2_RING_VGPRS : 96))
                                   ? KC / KS
                                   : ring_depth(NST, KS, NFR, CT >= 4 ? 64 : 96);
     // Single-image mode: when two ping-pong images (+ bias table) do not fit the 160 KB of LDS
