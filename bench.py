@@ -79,7 +79,7 @@ PMC_PER_LAUNCH = {"gznn::trunk_kernel_h2<128, 4, 3>": {
               "1024-row launches, tools/gpu_pmc_r04.sh): busy cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)"}}
 
 
-def per_game_cost(o, threads, slots, run_s, rate=None):
+def per_game_cost(o, threads, slots, run_s, rate=None, world=1):
     """Per-game cost by the game's ordinal within its slot (gz_ordinal_stats of rank 0's runner, the
     whole run): is a slot's k-th game dearer than its first?  Plus the first-game cohort (ordinal 1:
     one game per slot, every game an independent draw from the initial position with its own RNG
@@ -125,8 +125,10 @@ def per_game_cost(o, threads, slots, run_s, rate=None):
     # E[evals per game] from below (an upper bound on games/s), exactly once every first game completed.
     if rate and slots and c_e > 0:
         mean_e = c_e / slots
+        # rate and slots are per rank (every rank runs the same workload on its own game range):
+        # the aggregate is world x the per-rank figure
         cohort["games_per_sec_renewal"] = {
-            "value": rate / mean_e, "evals_per_game": mean_e,
+            "value": world * rate / mean_e, "per_rank": rate / mean_e, "ranks": world, "evals_per_game": mean_e,
             "kind": "renewal estimate: every slot's first game completed" if o["inflight_games_ord"][0] == 0
             else "upper bound: %d of %d first games still in progress (counted at their evaluations so far)"
                  % (o["inflight_games_ord"][0], slots)}
@@ -148,8 +150,6 @@ def parse():
     ap.add_argument("--age-games", type=float, default=3.0,
                     help="steady state: age the game population until this many games per game slot completed ...")
     ap.add_argument("--age-seconds", type=float, default=400.0, help="... or this many seconds passed (0: no aging)")
-    ap.add_argument("--exit-after-line", action="store_true",
-                    help="with --no-cpu-baseline on one GPU: exit right after the line, without stopping the runner")
     ap.add_argument("--threads", type=int, default=0, help="engine threads per GPU (0: the rank's CPU share)")
     ap.add_argument("--pools", type=int, default=2, help="game pools per engine thread")
     ap.add_argument("--batch", type=int, default=256)
@@ -158,10 +158,11 @@ def parse():
                     help="BASELINE.json configs[i-1]; 2 (breakthrough 8x8, 6x128) is the headline workload, "
                          "3-5 (reversi 10x128, hexLG13 12x256, amazons_10x10 20x256) run the same path")
     ap.add_argument("--mode", choices=["template", "literal"], default="template")
-    ap.add_argument("--precision", choices=["fp32", "bf16"], default=None,
-                    help="trunk arithmetic: fp32 = split hi/lo bf16 operands, three MFMAs per product "
-                         "(fp32-class accuracy, the reference runs fp32 TF; the default, every config); "
-                         "bf16 = bf16 operands")
+    ap.add_argument("--precision", choices=["bf16x3", "split", "bf16", "fp32"], default=None,
+                    help="trunk arithmetic: bf16x3 (alias split) = hi/lo bf16 operands, three MFMAs per "
+                         "product, fp32-class accuracy -- about 35x an IEEE fp32 forward's error on cfg2, "
+                         "NOT IEEE fp32 (the reference runs fp32 TF); the default, every config; "
+                         "bf16 = bf16 operands; fp32 = deprecated alias of bf16x3")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=45.0)
     ap.add_argument("--opening-seconds", type=float, default=30.0,
                     help="also report the GPU leg's rate over the first seconds of aging (the opening phase the "
@@ -365,8 +366,9 @@ def main():
     sm, transformer, desc = setup_game(args.config)
     if args.precision is None:
         # bf16x3 split on every BASELINE config (F = 256 on 13 x 13, cfg 4: the two-pass kernel)
-        args.precision = "fp32"
+        args.precision = "bf16x3"
     net = HipNet(desc, device, args.precision)
+    args.precision = net.precision   # canonical: "fp32" / "split" name bf16x3
     heads_fused = net.heads_fused()
 
     # weights: rank 0 creates, RCCL broadcast of the blob (the only collective on the path)
@@ -485,7 +487,7 @@ def main():
         # the trunk kernel runs as one of two variants by launch size; the roofline is reported for
         # the variant that took more trunk time, the other one alongside
         # the trunk kernels of small / large launches, as rocprofv3 names them (gz_net_kernel_name)
-        p = 3 if args.precision == "fp32" else 1
+        p = 3 if args.precision == "bf16x3" else 1
         k_large, k_small = net.kernel_name(True), net.kernel_name(False)
         if k_small == k_large:   # one trunk kernel for every launch size (single-image nets)
             variants = {k_large: (launches, rows, tms)}
@@ -612,18 +614,18 @@ def main():
                 gbps = out["roofline"]["traffic"] / (per_variant[dom]["avg_kernel_ms"] / 1e3) / 1e9
                 out["roofline"].update({"mfma_busy_frac": busy, "hbm_GBps": gbps, "hbm_peak_GBps": PEAK_HBM_GBPS,
                                         "hbm_frac": gbps / PEAK_HBM_GBPS, "pmc_source": pmc["source"]})
-        out["per_game_cost"] = per_game_cost(ordinals, threads, games_per_rank, run_s, rows / T / world if T > 0 else None)
+        out["per_game_cost"] = per_game_cost(ordinals, threads, games_per_rank, run_s, rows / T / world if T > 0 else None,
+                                             world)
     # The runner is stopped only now: every figure above comes from the snapshots taken at the end
-    # of the timed steps.  A stop waits for each engine thread's current poll, which can sit inside
-    # a long NN-free root spin (minutes on few-slot hexLG13 / amazons runs), so without a CPU leg
-    # the line is printed first.
+    # of the timed steps.  The stop is bounded (gz_runner_stop cancels the pools: an engine thread
+    # inside a long NN-free root spin returns at the game's next playout); its time goes in the line
+    # when the line is printed after it.
     line_first = rank == 0 and (world > 1 or args.no_cpu_baseline)
     if line_first:
         print(json.dumps(out), flush=True)
-        if args.exit_after_line:   # few-slot length runs: do not wait out the engine threads' spins
-            sys.stdout.flush()
-            os._exit(0)
+    t_stop = time.time()
     runner.stop()
+    out["runner_stop_s"] = time.time() - t_stop
     runner.close()   # frees the games' trees before the CPU baseline
     if rank == 0 and not line_first:
         out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, evals, args.mode, args.batch, args.config)

@@ -64,7 +64,24 @@ class GzNetDesc(ctypes.Structure):
 
 GZ_PRECISION_BF16 = 1
 GZ_PRECISION_SPLIT = 3
-PRECISIONS = {"bf16": GZ_PRECISION_BF16, "fp32": GZ_PRECISION_SPLIT}
+# "bf16x3" (alias "split"): each fp32 operand as bf16 hi + lo, three MFMAs per product, ~16
+# significant bits per operand -- fp32-CLASS, not IEEE fp32: on the headline cfg2 batch its error
+# against the float64 oracle is ~35x an IEEE fp32 forward's (nn/tolerance.py).  "fp32" is the
+# pre-round-6 name of the same mode, kept as a deprecated alias.
+PRECISIONS = {"bf16": GZ_PRECISION_BF16, "bf16x3": GZ_PRECISION_SPLIT, "split": GZ_PRECISION_SPLIT,
+              "fp32": GZ_PRECISION_SPLIT}
+
+
+def canonical_precision(precision):
+    """The arithmetic mode's canonical name ("bf16" or "bf16x3"); "split" and the deprecated "fp32"
+    name bf16x3."""
+    if precision not in PRECISIONS:
+        raise ValueError("precision %r: one of bf16, bf16x3 (alias split; fp32 is deprecated)" % (precision,))
+    if precision == "fp32":
+        import warnings
+        warnings.warn('precision "fp32" selects the bf16x3 split mode (three bf16 MFMAs per product, '
+                      'fp32-class, not IEEE fp32): use "bf16x3"', DeprecationWarning, stacklevel=3)
+    return "bf16" if PRECISIONS[precision] == GZ_PRECISION_BF16 else "bf16x3"
 
 
 _FP = ctypes.POINTER(ctypes.c_float)
@@ -151,14 +168,16 @@ def _fptr(a):
 
 class HipNet(object):
     """Owner of a gz_net handle: the MI355X forward of one network on one device.
-    precision: "bf16" (bf16 operands) or "fp32" (split hi/lo bf16 operands, three MFMAs per product:
-    fp32-class accuracy, include/gzero_nn.h GZ_PRECISION_SPLIT)."""
+    precision: "bf16" (bf16 operands) or "bf16x3" (alias "split"; hi/lo bf16 operands, three MFMAs
+    per product: fp32-class accuracy -- about 35x an IEEE fp32 forward's error on cfg2 -- not IEEE
+    fp32, include/gzero_nn.h GZ_PRECISION_SPLIT).  "fp32" is a deprecated alias of "bf16x3";
+    self.precision holds the canonical name."""
 
     def __init__(self, desc, device=0, precision="bf16"):
         self.lib = nn_lib()
         self.desc = desc
-        self.precision = precision
-        self._cdesc = make_net_desc(desc, PRECISIONS[precision])
+        self.precision = canonical_precision(precision)
+        self._cdesc = make_net_desc(desc, PRECISIONS[self.precision])
         self.handle = self.lib.gz_net_create(ctypes.byref(self._cdesc), device)
         if not self.handle:
             raise RuntimeError("gz_net_create failed: %s" % self.lib.gz_nn_last_error().decode())
@@ -404,6 +423,7 @@ _ENGINE_SIGS = {
     "gz_unique_states_destroy": (None, [_VP]),
     "gz_unique_states_clear": (ctypes.c_int, [_VP]),
     "gz_pool_clear_unique_states": (ctypes.c_int, [_VP]),
+    "gz_pool_cancel": (ctypes.c_int, [_VP]),
     "gz_pool_create": (_VP, [_VP, _VP, ctypes.c_int, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_long, _VP,
                              _FP, ctypes.POINTER(_FP), _FP]),
     "gz_pool_destroy": (None, [_VP]),

@@ -471,6 +471,11 @@ extern "C" int gz_pool_start(gz_pool* p, const gz_selfplay_config* conf) {
     p->impl->startSelfPlayers(&p->conf);
     return 0;
 }
+extern "C" int gz_pool_cancel(gz_pool* p) {
+    if (!p) return fail("null pool");
+    p->impl->cancel();
+    return 0;
+}
 extern "C" int gz_pool_poll(gz_pool* p, int pred_count) {
     p->impl->getPredictDoneEvent()->pred_count = pred_count;
     p->impl->poll();

@@ -82,7 +82,17 @@ namespace {
 enum SpinStat {
     kSdBuilds, kSdBuildOk, kSdFailRoot, kSdFailUnselectable, kSdFailVisited, kSdFailInflight, kSdFailWinNode,
     kSdFailWinScore, kSdFailLatch, kSdFailFewWins, kSdFailOrder, kSdFailWatched, kSdRegsPlayouts,
-    kSdSlowPlayouts, kSdOrdinaryPlayouts, kSdRetryWait, kSdSelect, kSdSelectSorted, kSdCount
+    kSdSlowPlayouts, kSdOrdinaryPlayouts, kSdRetryWait, kSdSelect, kSdSelectSorted,
+    // NN-free ordinary playouts by the root's finalised wins (0 / 1 / >= 2) and by where they end
+    kSdFree0, kSdFree1, kSdFree2, kSdFreeD2, kSdFreeD3, kSdFreeD4, kSdFreeD5, kSdFreeD6, kSdFreeConv,
+    kSdFreeX1Win,
+    // playoutMain's exits, and the NN-free playouts of moves ending at each
+    kSdExitFinal, kSdExitConvPlayouts, kSdExitConvEvals, kSdExitNonConvEvals, kSdExitOther,
+    kSdFreeAtConvPlayouts, kSdFreeAtConvEvals, kSdFreeAtNonConvEvals,
+    // register runs: how they end
+    kSdRegRuns, kSdRegFailNoise, kSdRegFailLatch, kSdRegFailSep, kSdRegExpired,
+    kSdLatchDraws,   // fast-path playouts that read a root-latch draw
+    kSdCount
 };
 struct SpinStats {
     const bool on = std::getenv("GZ_SPIN_STATS") != nullptr;
@@ -92,7 +102,12 @@ struct SpinStats {
         static const char* names[kSdCount] = {
             "builds", "build_ok", "fail_root", "fail_unselectable", "fail_visited", "fail_inflight",
             "fail_win_node", "fail_win_score", "fail_latch", "fail_few_wins", "fail_order", "fail_watched",
-            "regs_playouts", "slow_playouts", "ordinary_playouts", "retry_wait", "select", "select_sorted"};
+            "regs_playouts", "slow_playouts", "ordinary_playouts", "retry_wait", "select", "select_sorted",
+            "free_w0", "free_w1", "free_w2", "free_d2", "free_d3", "free_d4", "free_d5", "free_d6+", "free_converged",
+            "free_d3_forced_win",
+            "exit_finalised", "exit_conv_playouts", "exit_conv_evals", "exit_nonconv_evals", "exit_other",
+            "free_at_conv_playouts", "free_at_conv_evals", "free_at_nonconv_evals",
+            "reg_runs", "reg_fail_noise", "reg_fail_latch", "reg_fail_sep", "reg_expired", "latch_draws"};
         std::fprintf(stderr, "gz spin stats:");
         for (int i = 0; i < kSdCount; ++i) std::fprintf(stderr, " %s=%ld", names[i], c[i].load());
         std::fprintf(stderr, "\n");
@@ -1375,21 +1390,26 @@ bool PuctEvaluator::spinBuild() {
             std::memset(watched, 0, n);
             for (int w = 0; w < nwatch; ++w) watched[spin.watched_flag[w]] = 1;
             const uint16_t* order = S.sortedOrder(n);
-            int k = 0, kw = 0;
+            // each candidate's position among the children the selection loop reaches (all but the
+            // skipped bad-fallback ones): the index of its root-latch draw within a playout
+            int k = 0, kw = 0, pos = 0;
             for (int j = 0; j < n; ++j) {
                 const int i = order[j];
                 if (kind[i] == kWinC) {
                     spin.cand[k] = (uint16_t)i;
+                    spin.cand_pos[k] = (uint16_t)pos;
                     spin.cand_kind[k++] = SpinEpoch::kWin;
                     ++kw;
                 } else if (watched[i]) {
                     spin.cand[k] = (uint16_t)i;
+                    spin.cand_pos[k] = (uint16_t)pos;
                     spin.cand_kind[k++] = kind[i] == kUnexp ? SpinEpoch::kPrior : SpinEpoch::kScored;
                 }
+                if (kind[i] != kSkipC) ++pos;
             }
             // (a comparator that is not a strict weak ordering -- the reference's, with negative
             // scores next to unexpanded children -- may drop or repeat elements: ordinary path)
-            if (kw != nw || k != nw + nwatch) return sd(kSdFailOrder), false;
+            if (kw != nw || k != nw + nwatch || pos != reach) return sd(kSdFailOrder), false;
             spin.ncand = k;
             spin.nvisited = nvis;
             spin.watch_prior = watch_prior;
@@ -1563,8 +1583,14 @@ int PuctEvaluator::spinRunSlow(int limit, bool verify) {
         }
         float best_score = -1;
         int best = -1;
-        bool best_win = false, latched_win = false;
+        bool best_win = false;
         double best_exact = 0.0;
+        // the root latch (evaluator.cpp:461-475): with the latch active every reached child draws
+        // rng.get() in sorted order, and a child whose traversals exceed 0.66 v is left out of the
+        // selection when its draw exceeds 0.1.  Only wins can be latched inside an epoch (spinBuild);
+        // a latched win's draw is read at its position, the others are discarded unread.
+        const Rng rng0 = rng;
+        int drawn = 0;
         for (int k = 0; k < spin.ncand; ++k) {
             const int i = spin.cand[k];
             const uint8_t kind = spin.cand_kind[k];
@@ -1572,8 +1598,10 @@ int PuctEvaluator::spinRunSlow(int limit, bool verify) {
             const PuctNode* cn = c->to_node;
             if (kind == SpinEpoch::kWin && latch && c->traversals > 16 &&
                 c->traversals > node->visits * limit_latch_root) {
-                latched_win = true;
-                break;
+                if (drawn == 0) sd(kSdLatchDraws);
+                rng.discard((uint64_t)(spin.cand_pos[k] - drawn));
+                drawn = spin.cand_pos[k] + 1;
+                if (rng.get() > 0.1) continue;
             }
             const int traversals = c->traversals + 1;
             const double inflight_visits = cn != nullptr ? cn->inflight_visits : 0;
@@ -1593,21 +1621,21 @@ int PuctEvaluator::spinRunSlow(int limit, bool verify) {
                 best_exact = score;
             }
         }
-        // a win reaches the root latch, a watched candidate wins (its playout descends: ordinary
-        // path), or the result is not separated from the unwatched bound
-        if (latched_win || !best_win || !(spin.unwatched_bound < best_exact) ||
+        // a watched candidate wins (its playout descends: ordinary path), or the result is not
+        // separated from the unwatched bound
+        if (best < 0 || !best_win || !(spin.unwatched_bound < best_exact) ||
             !(spin.unwatched_bound <= (double)(float)best_exact)) {
+            rng = rng0;
             fail();
             break;
         }
         PuctNodeChild* chosen = cs + best;
+        if (latch) rng.discard((uint64_t)(spin.reach - drawn));   // the remaining draws (values unused)
 
         if (verify) {
             // the ordinary selection from the same RNG state must pick the same child
-            const Rng before = rng;
-            for (int j = 0; latch && j < spin.reach; ++j) (void)rng.get();
             const Rng after = rng;
-            rng = before;
+            rng = rng0;
             Path tmp;
             PuctNodeChild* ref = selectChild(node, tmp);
             if (ref != chosen || !(rng == after)) {
@@ -1619,8 +1647,6 @@ int PuctEvaluator::spinRunSlow(int limit, bool verify) {
                 std::abort();
             }
             count_verified();
-        } else if (latch) {
-            rng.discard((uint64_t)spin.reach);   // the root latch's per-child draws (values unused)
         }
 
         // treePlayout (evaluator.cpp:658-720): root -> chosen (finalised terminal), then backup()
@@ -1667,7 +1693,7 @@ int PuctEvaluator::spinRunSlow(int limit, bool verify) {
         }
         if (node->visits % 100 == 0) {
             // normaliseX inside an epoch: the epoch expires when the rescaling drifts (spinBuild)
-            float before[SpinEpoch::kMaxWins + SpinEpoch::kMaxWatched];
+            float before[SpinEpoch::kMaxWins + SpinEpoch::kMaxWatched] = {};
             for (int k = 0; k < spin.ncand; ++k) before[k] = cs[spin.cand[k]].policy_prob;
             node->normaliseX();
             double dev = 0.0;
@@ -1715,7 +1741,48 @@ struct SpinRegs {
     const uint16_t* cand = nullptr;  // candidate k's child index
     double drift = 1.0;              // the epoch's product of normalisation factors
     bool expired = false;            // a normalisation drifted: the epoch ends after this playout
+    int why = 0;                     // diagnostics (GZ_SPIN_STATS): 1 noise, 2 latch, 3 separation
+    Rng* rng = nullptr;              // the evaluator's generator (root-latch draws read inside a run)
+    uint16_t pos[kC];                // candidate k's position among the reached children (its draw)
 };
+
+// The root latch inside a register run (selectChild, evaluator.cpp:461-475): with the latch active
+// each reached child draws rng.get() in sorted order and a child whose traversals exceed 0.66 v is
+// left out of the selection when its draw exceeds 0.1.  Returns the mask of candidates left out of
+// this playout; the pending discards (earlier playouts' unread draws) and the draws before each
+// latched win are skipped, the playout's draws after the last latched one stay for the caller
+// (reach - *drawn).  On a failed playout the caller restores the generator from `saved`.
+struct LatchDraws {
+    Rng saved;
+    uint64_t saved_pending = 0;
+    bool drew = false;
+    int drawn = 0;
+};
+template <class TA>
+inline uint32_t latch_skips(SpinRegs& x, const TA& T, int nc, uint32_t v, uint64_t& pending, LatchDraws& ld) {
+    const float limit_latch_root = 0.66;
+    uint32_t mask = 0;
+    for (int k = 0; k < nc; ++k) {
+        const uint32_t t = (uint32_t)T[k];
+        if (!(x.WIN[k] && t > 16 && t > v * limit_latch_root)) continue;
+        if (!ld.drew) {
+            ld.saved = *x.rng;
+            ld.saved_pending = pending;
+            ld.drew = true;
+            sd(kSdLatchDraws);
+        }
+        x.rng->discard(pending + (uint64_t)(x.pos[k] - ld.drawn));
+        pending = 0;
+        ld.drawn = x.pos[k] + 1;
+        if (x.rng->get() > 0.1) mask |= 1u << k;
+    }
+    return mask;
+}
+inline void latch_undo(SpinRegs& x, uint64_t& pending, const LatchDraws& ld) {
+    if (!ld.drew) return;
+    *x.rng = ld.saved;
+    pending = ld.saved_pending;
+}
 
 // normaliseX at the root inside a register run (backup, evaluator.cpp:650): the candidates'
 // policies to the child entries, normalise, read them back; the epoch expires when the factor
@@ -1772,7 +1839,6 @@ __attribute__((noinline)) void spin_wins(SpinRegs& x, int limit) {
         for (int ii = 1; ii < R; ii++) r = lead == ii ? c[ii] : r;
         return r;
     };
-    const float limit_latch_root = 0.66;
     const float pc_root = x.pc_root;
     const bool noise_check = x.noise_check;
     const double ub = x.ub;
@@ -1801,20 +1867,15 @@ __attribute__((noinline)) void spin_wins(SpinRegs& x, int limit) {
         pc += pc_root;
         const double sqrt_node_visits = sqrt_pos(v + 1);
         const bool latch = v > 1000 && v < 40000000;
-        if (check_latch) {
-            bool latched_win = false;
-            for (int k = 0; k < NC; ++k) latched_win |= T[k] > 16 && T[k] > v * limit_latch_root;
-            if (latch && latched_win) {
-                failed = true;
-                break;
-            }
-        }
+        LatchDraws ld;
+        const uint32_t skip = check_latch && latch ? latch_skips(x, T, NC, v, discards, ld) : 0u;
         double child_score = win_base;
         child_score *= 1.0f + pc;
         float best_score = -1;
         int best = -1;
         double best_exact = 0.0;
         for (int k = 0; k < NC; ++k) {
+            if (skip >> k & 1) continue;
             const int traversals = T[k] + 1;
             const double inflight_visits = 0;
             const double exploration_score = pc * P[k] * sqrt_node_visits / (traversals + inflight_visits);
@@ -1826,10 +1887,11 @@ __attribute__((noinline)) void spin_wins(SpinRegs& x, int limit) {
             }
         }
         if (best < 0 || !(ub < best_exact) || !(ub <= (double)(float)best_exact)) {
+            latch_undo(x, discards, ld);
             failed = true;
             break;
         }
-        discards += latch ? reach : 0;
+        discards += latch ? reach - ld.drawn : 0;
         touched |= 1u << best;
         for (int ii = 0; ii < R; ii++) {
             float visits = v;
@@ -1891,7 +1953,6 @@ __attribute__((noinline, target("avx2"))) void spin_wins_v(SpinRegs& x, int limi
     const float sc0 = x.lsc[0][0], sc1 = x.lsc[0][1];
     float cur0 = x.cur[0], cur1 = x.cur[1];
     const int lead = x.lead;
-    const float limit_latch_root = 0.66;
     const float pc_root = x.pc_root;
     const bool noise_check = x.noise_check;
     const double ub = x.ub;
@@ -1918,17 +1979,11 @@ __attribute__((noinline, target("avx2"))) void spin_wins_v(SpinRegs& x, int limi
         pc += pc_root;
         const double sqrt_node_visits = sqrt_pos(v + 1);
         const bool latch = v > 1000 && v < 40000000;
-        if (check_latch) {
+        LatchDraws ld;
+        uint32_t skip = 0;
+        if (check_latch && latch) {
             _mm_store_si128((__m128i*)Ta, Tv);
-            bool latched_win = false;
-            for (int k = 0; k < NC; ++k) {
-                const uint32_t t = (uint32_t)Ta[k];
-                latched_win |= t > 16 && t > v * limit_latch_root;
-            }
-            if (latch && latched_win) {
-                failed = true;
-                break;
-            }
+            skip = latch_skips(x, Ta, NC, v, discards, ld);
         }
         double child_score = win_base;
         child_score *= 1.0f + pc;
@@ -1942,17 +1997,18 @@ __attribute__((noinline, target("avx2"))) void spin_wins_v(SpinRegs& x, int limi
         int best = -1;
         double best_exact = 0.0;
         for (int k = 0; k < NC; ++k) {
-            if (sa[k] > best_score) {
+            if (!(skip >> k & 1) && sa[k] > best_score) {
                 best = k;
                 best_score = sa[k];
                 best_exact = sa[k];
             }
         }
         if (best < 0 || !(ub < best_exact) || !(ub <= (double)(float)best_exact)) {
+            latch_undo(x, discards, ld);
             failed = true;
             break;
         }
-        discards += latch ? reach : 0;
+        discards += latch ? reach - ld.drawn : 0;
         touched |= 1u << best;
         {
             float visits = v;
@@ -2030,7 +2086,6 @@ __attribute__((noinline, target("avx2"))) void spin_wins_b(SpinRegs& x, int limi
     const float sc0 = x.lsc[0][0], sc1 = x.lsc[0][1];
     float cur0 = x.cur[0], cur1 = x.cur[1];
     const int lead = x.lead;
-    const float limit_latch_root = 0.66;
     const float pc_root = x.pc_root;
     const bool noise_check = x.noise_check;
     const double ub = x.ub;
@@ -2053,7 +2108,7 @@ __attribute__((noinline, target("avx2"))) void spin_wins_b(SpinRegs& x, int limi
     const __m256i jv = _mm256_set_epi32(7, 6, 5, 4, 3, 2, 1, 0);
     while (done < limit && v < v_end) {
         if (noise_check && (lead == 0 ? cur0 : cur1) <= 0.95) {
-            failed = true;
+            failed = true; x.why = 1;
             break;
         }
         // block length: the run's limits and the next root normalisation (after the playout that
@@ -2102,17 +2157,11 @@ __attribute__((noinline, target("avx2"))) void spin_wins_b(SpinRegs& x, int limi
             const uint32_t vj = v + j;
             pc = pcs[j];
             const bool latch = vj > 1000 && vj < 40000000;
-            if (check_latch) {
+            LatchDraws ld;
+            uint32_t skip = 0;
+            if (check_latch && latch) {
                 _mm_store_si128((__m128i*)Ta, Tv);
-                bool latched_win = false;
-                for (int k = 0; k < NC; ++k) {
-                    const uint32_t t = (uint32_t)Ta[k];
-                    latched_win |= t > 16 && t > vj * limit_latch_root;
-                }
-                if (latch && latched_win) {
-                    failed = true;
-                    break;
-                }
+                skip = latch_skips(x, Ta, NC, vj, discards, ld);
             }
             double child_score = win_base;
             child_score *= 1.0f + pc;
@@ -2125,17 +2174,18 @@ __attribute__((noinline, target("avx2"))) void spin_wins_b(SpinRegs& x, int limi
             int best = -1;
             double best_exact = 0.0;
             for (int k = 0; k < NC; ++k) {
-                if (sa[k] > best_score) {
+                if (!(skip >> k & 1) && sa[k] > best_score) {
                     best = k;
                     best_score = sa[k];
                     best_exact = sa[k];
                 }
             }
             if (best < 0 || !(ub < best_exact) || !(ub <= (double)(float)best_exact)) {
-                failed = true;
+                latch_undo(x, discards, ld);
+                failed = true; x.why = 3;
                 break;
             }
-            discards += latch ? reach : 0;
+            discards += latch ? reach - ld.drawn : 0;
             touched |= 1u << best;
             if (j == jchg) {   // this playout's update changes cur: taken, and its decay reads it
                 cur0 = n0s[j];
@@ -2181,11 +2231,10 @@ __attribute__((noinline, target("avx2"))) void spin_wins_b(SpinRegs& x, int limi
 
 // any candidate mix (wins and watched scored children)
 void spin_mixed(SpinRegs& x, int limit) {
-    const float limit_latch_root = 0.66;
     const int nc = x.nc, lead = x.lead, role_count = x.role_count;
     while (x.done < limit && x.v < x.v_end) {
         if (x.noise_check && x.cur[lead] <= 0.95) {
-            x.failed = true;
+            x.failed = true; x.why = 1;
             break;
         }
         const uint32_t v = x.v;
@@ -2197,12 +2246,10 @@ void spin_mixed(SpinRegs& x, int limit) {
         float best_score = -1;
         int best = -1;
         double best_exact = 0.0;
-        bool latched_win = false;
+        LatchDraws ld;
+        const uint32_t skip = latch ? latch_skips(x, x.T, nc, v, x.discards, ld) : 0u;
         for (int k = 0; k < nc; ++k) {
-            if (x.WIN[k] && latch && x.T[k] > 16 && x.T[k] > v * limit_latch_root) {
-                latched_win = true;
-                break;
-            }
+            if (skip >> k & 1) continue;
             const int traversals = x.T[k] + 1;
             const double inflight_visits = 0;
             double exploration_score = pc * x.P[k] * sqrt_node_visits / (traversals + inflight_visits);
@@ -2216,11 +2263,12 @@ void spin_mixed(SpinRegs& x, int limit) {
                 best_exact = score;
             }
         }
-        if (latched_win || best < 0 || !x.WIN[best] || !(x.ub < best_exact) || !(x.ub <= (double)(float)best_exact)) {
-            x.failed = true;
+        if (best < 0 || !x.WIN[best] || !(x.ub < best_exact) || !(x.ub <= (double)(float)best_exact)) {
+            latch_undo(x, x.discards, ld);
+            x.failed = true; x.why = 3;
             break;
         }
-        if (latch) x.discards += x.reach;
+        if (latch) x.discards += x.reach - ld.drawn;
         x.touched |= 1u << best;
         x.LV[best]++;
         for (int ii = 0; ii < role_count; ii++) {
@@ -2287,6 +2335,8 @@ int PuctEvaluator::spinRunRegs(int limit) {
     x.node = node;
     x.cand = spin.cand;
     x.drift = spin.drift;
+    x.rng = &rng;
+    for (int k = 0; k < nc; ++k) x.pos[k] = spin.cand_pos[k];
     // Register loops for all-win epochs: GZ_SPIN_VEC=2 (default) the AVX2 loop in blocks of eight
     // playouts, =1 the AVX2 loop per playout, =0 the scalar loop (all compute the same playouts).
     // On the GPU box's EPYC 9575F the AVX2 loops ran +4.7 % leaf-evals/s over the scalar one in the
@@ -2331,6 +2381,11 @@ int PuctEvaluator::spinRunRegs(int limit) {
         else spin.fail_next = true;
     }
     sd(kSdRegsPlayouts, done);
+    if (__builtin_expect(g_spin_stats.on, 0)) {
+        sd(kSdRegRuns);
+        if (x.failed) sd(x.why == 1 ? kSdRegFailNoise : x.why == 2 ? kSdRegFailLatch : kSdRegFailSep);
+        if (x.expired) sd(kSdRegExpired);
+    }
     return done;
 }
 
@@ -2370,12 +2425,27 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
         const bool spin_epoch = spin.valid && spin.conv_false && spin.root == root && root->visits < spin.v_end;
         const bool is_converged = need_converged && !spin_epoch ? converged(conf->converged_visits) : false;
 
-        if (end_time > 0 && get_time() > end_time) break;
-        if (root->is_finalised && stats.num_tree_playouts > 100) break;
-        if (is_converged && stats.num_tree_playouts > max_tree_playouts) break;
-        if (number_of_nodes > 50000000) break;
-        if (is_converged && stats.num_evaluations > max_evaluations) break;
-        if (!is_converged && stats.num_evaluations > max_non_converged_evaluations) break;
+        // (diagnostics: GZ_SPIN_STATS counts the exits and the NN-free playouts of their moves)
+        auto exit_stat = [&](SpinStat e, SpinStat f) {
+            if (__builtin_expect(!g_spin_stats.on, 1)) return;
+            sd(e);
+            if (f != kSdCount) sd(f, stats.num_tree_playouts - stats.num_evaluations);
+        };
+        if (end_time > 0 && get_time() > end_time) { exit_stat(kSdExitOther, kSdCount); break; }
+        if (root->is_finalised && stats.num_tree_playouts > 100) { exit_stat(kSdExitFinal, kSdCount); break; }
+        if (is_converged && stats.num_tree_playouts > max_tree_playouts) {
+            exit_stat(kSdExitConvPlayouts, kSdFreeAtConvPlayouts);
+            break;
+        }
+        if (number_of_nodes > 50000000) { exit_stat(kSdExitOther, kSdCount); break; }
+        if (is_converged && stats.num_evaluations > max_evaluations) {
+            exit_stat(kSdExitConvEvals, kSdFreeAtConvEvals);
+            break;
+        }
+        if (!is_converged && stats.num_evaluations > max_non_converged_evaluations) {
+            exit_stat(kSdExitNonConvEvals, kSdFreeAtNonConvEvals);
+            break;
+        }
         if (use_think_time) {
             if (is_converged && elapsed(conf->think_time)) break;
             if (!is_converged && elapsed(conf->think_time * conf->evaluation_multiplier_to_convergence)) break;
@@ -2400,14 +2470,30 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
         if (ran == 0) {
             spin.valid = false;
             path.clear();
+            const int ev0 = stats.num_evaluations;
             depth = treePlayout(root, path);
             ran = 1;
             sd(kSdOrdinaryPlayouts);
+            if (__builtin_expect(g_spin_stats.on, 0) && stats.num_evaluations == ev0) {
+                int nw = 0;
+                for (int i = 0; i < root->num_children; ++i) {
+                    const PuctNode* cn = root->getNodeChild(0, i)->to_node;
+                    if (cn != nullptr && cn->is_finalised && cn->getCurrentScore(root->lead_role_index) > 0.99) ++nw;
+                }
+                sd(nw == 0 ? kSdFree0 : nw == 1 ? kSdFree1 : kSdFree2);
+                sd(depth <= 2 ? kSdFreeD2 : depth == 3 ? kSdFreeD3 : depth == 4 ? kSdFreeD4 : depth == 5 ? kSdFreeD5 : kSdFreeD6);
+                if (depth == 3 && path[2].node->is_finalised && path[1].node->lead_role_index >= 0 &&
+                    path[2].node->getCurrentScore(path[1].node->lead_role_index) > 0.99)
+                    sd(kSdFreeX1Win);
+                if (convergedExact(conf->converged_visits)) sd(kSdFreeConv);
+            }
         }
         stats.playouts_max_depth = std::max(depth, stats.playouts_max_depth);
         stats.playouts_total_depth += depth * ran;
 
-        if (conf->spin_yield_playouts > 0) {
+        if (__builtin_expect(scheduler->cancelled(), 0)) {
+            scheduler->yield();   // teardown: the main loop stops there (NetworkScheduler::cancel)
+        } else if (conf->spin_yield_playouts > 0) {
             if (stats.num_evaluations != evals_seen) {   // (never after a spin run)
                 evals_seen = stats.num_evaluations;
                 quiet_playouts = 0;

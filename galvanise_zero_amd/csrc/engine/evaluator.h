@@ -112,6 +112,7 @@ private:
         int ncand = 0;               // wins + watched candidates, in sortedChildrenSelect order
         uint16_t cand[kMaxWins + kMaxWatched];
         uint8_t cand_kind[kMaxWins + kMaxWatched];
+        uint16_t cand_pos[kMaxWins + kMaxWatched];   // position among the reached children (latch draw)
         uint16_t watched_flag[kMaxWatched];
         int nvisited = 0;            // children with visits > 0, in child order (FPU policy sum)
         uint16_t visited[kMaxVisited];

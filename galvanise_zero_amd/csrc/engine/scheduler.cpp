@@ -99,6 +99,7 @@ void NetworkScheduler::prefetch_reply(int idx) const {
 // scheduler.cpp:132-205
 void NetworkScheduler::mainLoop() {
     while (true) {
+        if (cancelled()) break;
         bool jump_to_top = false;
         if (runnables.empty()) {
             if (requestors.empty()) {
@@ -115,6 +116,7 @@ void NetworkScheduler::mainLoop() {
 
         if (jump_to_top) {
             coro_switch_to(top);
+            if (cancelled()) break;
             GZ_ASSERT(predict_done_event->pred_count == (int)requestors.size());
             if (!requestors.empty()) {
                 // replies in request order; the next request's node (header and child array, which
@@ -144,6 +146,11 @@ void NetworkScheduler::mainLoop() {
 
 // scheduler.cpp:207-241
 void NetworkScheduler::poll(const PredictDoneEvent* pde, ReadyEvent* ready_event) {
+    ready_event->channel_buf = channel_buf;
+    if (main_loop == nullptr && cancelled()) {   // cancelled earlier: nothing runs any more
+        ready_event->buf_count = 0;
+        return;
+    }
     GZ_ASSERT(main_loop != nullptr);
     top = coro_current();
     main_loop->parent = top;
@@ -152,12 +159,12 @@ void NetworkScheduler::poll(const PredictDoneEvent* pde, ReadyEvent* ready_event
     coro_switch_to(main_loop);
     predict_done_event = nullptr;
 
+    if (main_loop->dead && cancelled()) channel_buf_indx = 0;   // stopped by cancel(): no batch
     if (channel_buf_indx == 0) {
         GZ_ASSERT(main_loop->dead);
         coro_destroy(main_loop);
         main_loop = nullptr;
     }
-    ready_event->channel_buf = channel_buf;
     ready_event->buf_count = channel_buf_indx;
 }
 

@@ -12,6 +12,7 @@
 #include "coro.h"
 #include "node.h"
 
+#include <atomic>
 #include <deque>
 #include <functional>
 #include <vector>
@@ -49,6 +50,13 @@ public:
     int batchSize() const { return batch_size; }
     float* channelBuf() { return channel_buf; }
 
+    // Cancellation (the owner's teardown; any thread): the main loop stops at its next turn -- a
+    // game coroutine reaches it at its next evaluation or yield, and playoutMain yields every
+    // playout once cancelled -- and poll() then returns no rows, at once for every later call.  The
+    // suspended games are abandoned (freed with the scheduler); nothing they emitted changes.
+    void cancel() { cancelled_.store(true, std::memory_order_relaxed); }
+    bool cancelled() const { return cancelled_.load(std::memory_order_relaxed); }
+
 private:
     void mainLoop();
     void prefetch_reply(int idx) const;
@@ -70,6 +78,7 @@ private:
     int channel_buf_indx = 0;
 
     const PredictDoneEvent* predict_done_event = nullptr;
+    std::atomic<bool> cancelled_{false};
 };
 
 }  // namespace gz

@@ -168,6 +168,8 @@ public:
 
     void startSelfPlayers(const SelfPlayConfig* config);
     void poll();
+    // teardown from any thread: the pool's poll returns promptly with no rows (NetworkScheduler::cancel)
+    void cancel() { scheduler->cancel(); }
 
     // games in progress by ordinal (OrdinalStats::kOrdinals buckets): count, engine seconds and
     // evaluations they have used so far

@@ -178,6 +178,10 @@ SelfPlayWorker::SelfPlayWorker(Supervisor* sup, SelfPlayManager* man0, SelfPlayM
 
 SelfPlayWorker::~SelfPlayWorker() {
     stop = true;
+    // a pool can spin for minutes without an evaluation (the reference's playoutMain): cancel both
+    // so that a poll in progress returns at its games' next yield instead of at their next batch
+    man0->cancel();
+    man1->cancel();
     inbound.wake();
     if (thread.joinable()) thread.join();
     delete man0;

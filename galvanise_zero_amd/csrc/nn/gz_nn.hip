@@ -204,7 +204,12 @@ extern "C" gz_net* gz_net_create(const gz_net_desc* desc, int device) {
                fused_heads_bytes(np, d.role_count, heads_row(d.role_count, d.policy_dist_count, d.value_hidden_size),
                                  gap_features(d), c.nb, 1, fpad) <= c.act_bytes;
     };
-    if (kl.fn && !wg_fits(kl)) kl = KernelChoice{};
+    if (kl.fn && !wg_fits(kl)) {
+        // the wave-group default (23) does not fit this geometry's scratch: the two-board 4-wave
+        // kernel (21, one image per workgroup) before the one-board one
+        kl = vl == kLargeVariant ? select_kernel(fpad, pt, kLargeFallback, precision, v2) : KernelChoice{};
+        if (kl.fn && !wg_fits(kl)) kl = KernelChoice{};
+    }
     if (kc.fn && !wg_fits(kc)) kc = KernelChoice{};
     if (kc.fn && !kl.fn && vl != vs) {   // geometries with a single (one board per workgroup) variant
         kl = kc;
@@ -917,6 +922,11 @@ extern "C" int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_
     if (P.consumed != count) return fail("internal: blob plan mismatch");
     const ImageLayout I = image_layout(net);
     HIPCHK(hipSetDevice(net->device));
+    // The blob's producer (an RCCL broadcast, a copy on torch's stream, ...) ran on some other
+    // stream: net->stream is non-blocking, so nothing orders the fold / pack kernels after it.  Wait
+    // for all work issued to the device so far (a roll is rare; the runner applies it between
+    // launches, whose in-flight ones gz_net_set_weights waits for anyway).
+    HIPCHK(hipDeviceSynchronize());
     hipStream_t st = net->stream;
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));

@@ -793,6 +793,12 @@ extern "C" int gz_runner_stats_get(gz_runner* r, gz_runner_stats* out) {
 extern "C" int gz_runner_stop(gz_runner* r) {
     r->stop = true;
     r->qcv.notify_all();
+    // an engine thread inside gz_pool_poll returns at its pool's next coroutine switch: a game that
+    // spins without evaluations (playoutMain, evaluator.cpp:744-886) would otherwise hold it until
+    // the spin ends -- minutes on few-slot or deep-config runners.  The games in progress are
+    // abandoned (a stopped runner cannot be restarted); samples already emitted are unchanged.
+    for (Pool& p : r->pools)
+        if (p.pool) gz_pool_cancel(p.pool);
     for (std::thread& th : r->threads) th.join();
     r->threads.clear();
     if (r->launcher.joinable()) r->launcher.join();   // drains the batches in flight

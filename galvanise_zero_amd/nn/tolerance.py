@@ -20,6 +20,13 @@ tests/test_bench_shape_gpu.py, tests/test_nn_gpu.py::test_split_precision_agains
 __graft_entry__.smoke() assert these constants (test_deep_config_bench_weights asserts each config's
 logits bound on its own, cfg2 included).
 
+What the arithmetic is: bf16x3 ("split"; HipNet / bench.py --precision "bf16x3", the old name "fp32"
+is a deprecated alias) keeps ~16 significant bits per operand against IEEE fp32's 24, with fp32
+accumulation and an fp32 residual stream.  It is fp32-CLASS, not fp32: on the headline cfg2 batch
+(1,024 rows, tests/test_nn_gpu.py::test_split_precision_against_fp32) its max error against the
+float64 oracle is 1.5-2.0e-4, about 35x the 5.7e-6 of an IEEE fp32 forward of the same net (torch
+fp32 on the CPU), and 300x below bf16's 5.9e-2.
+
 The north-star tolerance per config, then:
   cfg2, cfg3   the probability bounds below (max / mean / KL), on the bench's weights
   cfg4, cfg5   the relative logits bound below on the bench's (saturating) weights, and in probability

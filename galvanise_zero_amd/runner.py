@@ -164,6 +164,12 @@ class GamePool(object):
             raise RuntimeError("gz_pool_poll: %s" % _native.engine_error())
         return n
 
+    def cancel(self):
+        """Teardown from any thread (gz_pool_cancel): a poll in progress returns 0 rows at the pool's
+        next coroutine switch, and so does every later poll."""
+        if self.lib.gz_pool_cancel(self.handle) != 0:
+            raise RuntimeError("gz_pool_cancel: %s" % _native.engine_error())
+
     def fetch_samples(self):
         s = _native.take_string(self.lib.gz_pool_fetch_samples(self.handle))
         return json.loads(s) if s else []

@@ -200,6 +200,13 @@ gz_pool* gz_pool_create(const gz_sm* sm, const gz_transformer* t, int batch_size
 void gz_pool_destroy(gz_pool* p);
 int gz_pool_start(gz_pool* p, const gz_selfplay_config* conf);
 int gz_pool_poll(gz_pool* p, int pred_count);   /* returns rows of planes now in planes_buf */
+/* Teardown, callable from any thread while another thread is inside gz_pool_poll: the poll in
+ * progress returns 0 rows at the pool's next coroutine switch (a game's next evaluation or yield;
+ * a game that spins without evaluations yields after every playout once cancelled), and so does
+ * every later poll.  The games in progress are abandoned (freed by gz_pool_destroy); samples
+ * already emitted are unchanged.  The reference tears its workers down with the process
+ * (supervisor.cpp:36); a runner hosting live rolls needs a bounded stop instead. */
+int gz_pool_cancel(gz_pool* p);
 int gz_pool_get_stats(gz_pool* p, gz_pool_stats* out);
 /* clears the pool's own duplicate filter (no-op for a pool created with a shared one) */
 int gz_pool_clear_unique_states(gz_pool* p);

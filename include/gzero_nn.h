@@ -86,7 +86,10 @@ int gz_net_set_weights(gz_net* net, const float* blob, size_t count);
 /* Upload weights from a *device* float32 blob (e.g. after an RCCL broadcast into device memory): the
  * BN fold and the bf16 (hi / lo) packing run as HIP kernels reading the blob in place -- no PCIe
  * round trip -- and produce the byte-identical image gz_net_set_weights builds on the host.  The
- * generation roll of a live runner (gz_runner_update_network with device_blob = 1) takes this path. */
+ * generation roll of a live runner (gz_runner_update_network with device_blob = 1) takes this path.
+ * The blob may still be in flight on any stream (a broadcast, an async copy): the call first waits
+ * for all work issued to the device (hipDeviceSynchronize), so no caller-side synchronisation is
+ * needed. */
 int gz_net_set_weights_device(gz_net* net, const float* d_blob, size_t count);
 /* device milliseconds of the last gz_net_set_weights_device (fold + pack kernels and copies) */
 double gz_net_last_roll_ms(const gz_net* net);

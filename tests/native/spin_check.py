@@ -1,6 +1,9 @@
 """Subprocess body of tests/test_puct_parity.py::test_spin_fast_path_*: plays breakthrough self-play
-through one pool (oracle CPU forward) and prints a digest of every sample plus the pool counters.
-The environment (GZ_SPIN_FAST, GZ_VERIFY_FASTPATH) is read once per process by the engine."""
+through one pool (oracle CPU forward, or with a 5th argument "fake" a cheap synthetic network -- a fixed
+random projection of each row's planes to logits and values, a deterministic function of the row -- so
+that a run reaches the deep spin regime at 800 evals/move) and prints a digest of every sample plus the
+pool counters.  The environment (GZ_SPIN_FAST, GZ_VERIFY_FASTPATH) is read once per process by the
+engine."""
 import hashlib
 import json
 import os
@@ -11,7 +14,20 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def main(game, games, polls, evals):
+def fake_forward(desc, planes):
+    import numpy as np
+    rng = np.random.default_rng(77)
+    x = planes.reshape(planes.shape[0], -1).astype(np.float64)
+    outs = []
+    for p in list(desc.policy_dist_count) + [desc.num_values]:
+        w = rng.standard_normal((x.shape[1], p)) * 0.2
+        z = np.tanh(x @ w) * 3.0
+        z = np.exp(z - z.max(axis=1, keepdims=True))
+        outs.append((z / z.sum(axis=1, keepdims=True)).astype(np.float32))
+    return outs
+
+
+def main(game, games, polls, evals, net="oracle"):
     from galvanise_zero_amd.defs import templates
     from galvanise_zero_amd.runner import GamePool
     from puct_harness import Setup
@@ -23,7 +39,10 @@ def main(game, games, polls, evals):
     n, digest, count = 0, hashlib.sha256(), 0
     for _ in range(polls):
         n = pool.poll(n)
-        outs = nn_ref.forward(setup.desc, setup.weights, pool.planes[:n])
+        if net == "fake":
+            outs = fake_forward(setup.desc, pool.planes[:n])
+        else:
+            outs = nn_ref.forward(setup.desc, setup.weights, pool.planes[:n])
         for dst, src in zip(pool.policies + [pool.values], outs):
             dst[:n] = src
         for s in pool.fetch_samples():
@@ -36,4 +55,4 @@ def main(game, games, polls, evals):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), *sys.argv[5:6])

@@ -45,8 +45,8 @@ def test_library_loads_and_resolves(header, lib):
         assert getattr(so, name) is not None
 
 
-@pytest.mark.parametrize("hw,precision,ok", [((21, 21), "bf16", False), ((19, 19), "fp32", True), ((19, 19), "bf16", True),
-                                              ((13, 13), "fp32", True)])
+@pytest.mark.parametrize("hw,precision,ok", [((21, 21), "bf16", False), ((19, 19), "bf16x3", True), ((19, 19), "bf16", True),
+                                              ((13, 13), "bf16x3", True)])
 def test_net_geometry_check(hw, precision, ok):
     """gz_net_create checks the board against the compiled kernels before any HIP call (so this runs
     without a GPU): boards up to 19 x 19 (23 position tiles) are accepted -- the reference's hex19
@@ -67,3 +67,20 @@ def test_net_geometry_check(hw, precision, ok):
         assert "unsupported network geometry" not in err, err
     else:
         assert not h and "unsupported network geometry F=80 H=21 W=21" in err, err
+
+
+def test_precision_names():
+    """The split mode is named for what it computes: "bf16x3" (alias "split"),
+    three bf16 MFMAs per product -- fp32-class, not IEEE fp32; the pre-round-6 name "fp32" still
+    selects it, with a DeprecationWarning.  Both map to the same gz_net_desc.precision."""
+    import warnings
+    assert _native.PRECISIONS["bf16x3"] == _native.PRECISIONS["split"] == _native.PRECISIONS["fp32"] \
+        == _native.GZ_PRECISION_SPLIT != _native.PRECISIONS["bf16"]
+    assert _native.canonical_precision("bf16x3") == _native.canonical_precision("split") == "bf16x3"
+    assert _native.canonical_precision("bf16") == "bf16"
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert _native.canonical_precision("fp32") == "bf16x3"
+    assert any(issubclass(x.category, DeprecationWarning) and "bf16x3" in str(x.message) for x in w)
+    with pytest.raises(ValueError):
+        _native.canonical_precision("fp16")

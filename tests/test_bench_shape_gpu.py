@@ -82,7 +82,7 @@ def test_headline_trunk_at_bench_shape(hip_device):
     from galvanise_zero_amd._native import HipNet
     desc = BASELINE_CONFIGS[2]["desc"]
     w = random_weights(desc, 7921)                     # bench.py's weights
-    net = HipNet(desc, hip_device, "fp32")
+    net = HipNet(desc, hip_device, "bf16x3")
     net.set_weights(to_blob(w))
     sizes = [215, 198, 256, 231, 203]
     x = random_planes(desc, sum(sizes), 20251103)
@@ -107,7 +107,7 @@ def test_headline_trunk_at_bench_shape(hip_device):
         r0 += k
 
 
-DEEP = {"cfg2": (2, "fp32", 256), "cfg3": (3, "fp32", 256), "cfg4": (4, "bf16", 256), "cfg4_split": (4, "fp32", 256), "cfg5": (5, "fp32", 256),
+DEEP = {"cfg2": (2, "bf16x3", 256), "cfg3": (3, "bf16x3", 256), "cfg4": (4, "bf16", 256), "cfg4_split": (4, "bf16x3", 256), "cfg5": (5, "bf16x3", 256),
         "cfg5_bf16": (5, "bf16", 256)}
 
 
@@ -155,7 +155,7 @@ def test_deep_config_damped_at_launch_shape(name, hip_device):
     cfg, sizes = DAMPED[name]
     desc = BASELINE_CONFIGS[cfg]["desc"]
     w = random_weights(desc, 7919, bias_std=0.2, res_gamma=0.15)
-    net = HipNet(desc, hip_device, "fp32")
+    net = HipNet(desc, hip_device, "bf16x3")
     net.set_weights(to_blob(w))
     x = random_planes(desc, sum(sizes), 20251200 + cfg)
     got = _segmented_forward(net, desc, x, sizes)

@@ -168,7 +168,7 @@ def _kl(ref, got):
 @pytest.mark.parametrize("name", SPLIT)
 def test_forward_parity_fp32(name, hip_device):
     desc = VARIANTS[name]
-    net, w = _net_p(desc, 7919, hip_device, name, "fp32")
+    net, w = _net_p(desc, 7919, hip_device, name, "bf16x3")
     for n in ((1, 7, 19) if name in BIG else (1, 7, 64)):
         x = random_planes(desc, n, 100 + n)
         got = net.forward(x)
@@ -189,7 +189,7 @@ def test_fp32_tolerance_detects_one_bf16_ulp(hip_device):
     desc = VARIANTS["cfg2"]
     w = random_weights(desc, 7919, bias_std=0.2)
     wp = [(k, v * np.float32(1 + 2.0 ** -8) if k == "res2_conv1" else v) for k, v in w]
-    net = HipNet(desc, hip_device, "fp32")
+    net = HipNet(desc, hip_device, "bf16x3")
     net.set_weights(to_blob(wp))
     x = random_planes(desc, 64, 164)
     errs = [_err(g, r)[0] for g, r in zip(net.forward(x), nn_ref.forward(desc, w, x))]
@@ -200,7 +200,7 @@ def test_fp32_tolerance_detects_one_bf16_ulp(hip_device):
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
 def test_batch_invariance_fp32(name, hip_device):
     desc = VARIANTS[name]
-    net, _ = _net_p(desc, 3, hip_device, name, "fp32")
+    net, _ = _net_p(desc, 3, hip_device, name, "bf16x3")
     x = random_planes(desc, 300, 9)
     full = net.forward(x)
     perm = np.random.default_rng(0).permutation(300)[:37]
@@ -234,7 +234,7 @@ def test_template_geometries(game, hint, hip_device):
     w = random_weights(desc, 7919, bias_std=0.2, res_gamma=0.15 if desc.residual_layers > 6 else 1.0)
     x = random_planes(desc, 9, 31)
     ref = nn_ref.forward(desc, w, x)
-    modes = [("bf16", TOL_BF16_GEOM), ("fp32", TOL_FP32)]   # (split beyond 8 x 8: the two-pass kernel)
+    modes = [("bf16", TOL_BF16_GEOM), ("bf16x3", TOL_FP32)]   # (split beyond 8 x 8: the two-pass kernel)
     for precision, tol in modes:
         net = HipNet(desc, hip_device, precision)
         net.set_weights(to_blob(w))
@@ -255,11 +255,11 @@ def test_kernel_variants_identical_fp32(variant, hip_device, monkeypatch):
     desc = VARIANTS["cfg2"]
     x = random_planes(desc, 33, 4)
     w = to_blob(random_weights(desc, 5, bias_std=0.2))
-    net = HipNet(desc, hip_device, "fp32")
+    net = HipNet(desc, hip_device, "bf16x3")
     net.set_weights(w)
     base = net.forward(x)
     monkeypatch.setenv("GZ_KERNEL_VARIANT", variant)
-    vnet = HipNet(desc, hip_device, "fp32")
+    vnet = HipNet(desc, hip_device, "bf16x3")
     vnet.set_weights(w)
     for a, b in zip(base, vnet.forward(x)):
         assert np.array_equal(a, b)
@@ -279,7 +279,7 @@ def test_wave_group_kernel_identical_at_bench_size(variant, n, hip_device, monke
     outs = []
     for v in ("21", variant):
         monkeypatch.setenv("GZ_KERNEL_VARIANT", v)
-        net = HipNet(desc, hip_device, "fp32")
+        net = HipNet(desc, hip_device, "bf16x3")
         net.set_weights(w)
         outs.append(net.forward(x))
     for a, b in zip(*outs):
@@ -301,10 +301,10 @@ def test_split_precision_against_fp32(hip_device):
     ref = nn_ref.forward(desc, w, x)
     t32 = TorchCPUNet(desc, w).predict_on_batch(x)
     errs = {"fp32 (torch-CPU)": [np.abs(np.asarray(g, np.float64) - r).max() for g, r in zip(t32, ref)]}
-    for precision in ("fp32", "bf16"):
+    for precision in ("bf16x3", "bf16"):
         net = HipNet(desc, hip_device, precision)
         net.set_weights(to_blob(w))
-        errs["split" if precision == "fp32" else "bf16"] = [np.abs(g - r).max() for g, r in zip(net.forward(x), ref)]
+        errs["split" if precision == "bf16x3" else "bf16"] = [np.abs(g - r).max() for g, r in zip(net.forward(x), ref)]
     for k, v in errs.items():
         print("precision %-18s max |err| vs float64 oracle per output: %s" % (k, " ".join("%.3g" % e for e in v)))
     split, f32, b16 = max(errs["split"]), max(errs["fp32 (torch-CPU)"]), max(errs["bf16"])
@@ -320,10 +320,10 @@ def test_split_precision_against_fp32(hip_device):
 # bf16 values; its chunk swizzle must stay inside the row for every K0 (rounds 1-4 sent chunks of
 # K0 = 96 / 160 / 224 rows into the next position's, which the loose bf16 tolerances hid)
 # 3 x the worst measured (profiles/r05c_large_board_errors.log): bf16 2.4e-3 / 9.1e-4, split 5.6e-6 / 2.6e-6
-TOL_K0 = {"bf16": (7.3e-3, 2.8e-3), "fp32": (1.7e-5, 7.9e-6)}
+TOL_K0 = {"bf16": (7.3e-3, 2.8e-3), "bf16x3": (1.7e-5, 7.9e-6)}
 
 
-@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16", "bf16x3"])
 @pytest.mark.parametrize("hw", [8, 13])
 @pytest.mark.parametrize("C", [3, 5, 9, 12, 15, 24])
 def test_initial_conv_widths(C, hw, precision, hip_device):
@@ -333,7 +333,7 @@ def test_initial_conv_widths(C, hw, precision, hip_device):
     try:
         net = HipNet(desc, hip_device, precision)
     except RuntimeError as e:   # 24 planes on 13 x 13 in split precision: the im2col staging exceeds the LDS
-        assert (C, hw, precision) == (24, 13, "fp32") and "LDS" in str(e), e
+        assert (C, hw, precision) == (24, 13, "bf16x3") and "LDS" in str(e), e
         return
     net.set_weights(to_blob(w))
     x = random_planes(desc, 7, 100)

@@ -77,7 +77,7 @@ def test_v2_model_files(key, hip_device):
         _check(key, desc, w, x, hip_device, "bf16", TOL_V2_BF16)
         # split precision on every board: two boards per workgroup up to 8 x 8, beyond that one board
         # per workgroup with two passes per conv (P = 2)
-        _check(key, desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
+        _check(key, desc, w, x, hip_device, "bf16x3", TOL_FP32, TOL_FP32_KL)
 
 
 GEOM_GAMES = ["breakthroughSmall", "breakthrough", "reversi", "hexLG13", "amazons_10x10"]
@@ -101,7 +101,7 @@ def test_v2_templates(game, hint, hip_device):
     w = random_weights(desc, 7919, bias_std=0.2, res_gamma=RES_GAMMA)
     x = random_planes(desc, 9, 31)
     _check("%s/%s" % (game, hint), desc, w, x, hip_device, "bf16", TOL_V2_BF16)
-    _check("%s/%s" % (game, hint), desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
+    _check("%s/%s" % (game, hint), desc, w, x, hip_device, "bf16x3", TOL_FP32, TOL_FP32_KL)
 
 
 V2_NETS = {"b1_58": FILES["breakthroughSmall/models/b1_58.json"], "f2_308": FILES["reversi_8x8/models/f2_308.json"],
@@ -109,7 +109,7 @@ V2_NETS = {"b1_58": FILES["breakthroughSmall/models/b1_58.json"], "f2_308": FILE
                                value_bn=True)}
 
 
-@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16", "bf16x3"])
 @pytest.mark.parametrize("name", sorted(V2_NETS))
 def test_v2_batch_invariance(name, precision, hip_device):
     """The squeeze-excite means are per board: rows do not depend on batch composition / slot, in
@@ -127,8 +127,8 @@ def test_v2_batch_invariance(name, precision, hip_device):
         assert np.array_equal(a[5:6], b)
 
 
-@pytest.mark.parametrize("precision,variant", [("bf16", "11"), ("bf16", "21"), ("bf16", "12"), ("fp32", "11"),
-                                               ("fp32", "21")])
+@pytest.mark.parametrize("precision,variant", [("bf16", "11"), ("bf16", "21"), ("bf16", "12"), ("bf16x3", "11"),
+                                               ("bf16x3", "21")])
 def test_v2_kernel_variants_identical(precision, variant, hip_device, monkeypatch):
     from galvanise_zero_amd._native import HipNet
     desc = V2_NETS["f2_308"]
@@ -189,13 +189,13 @@ def test_v2_concat_all_layers(name, hip_device):
     for n in (1, 300):
         x = random_planes(desc, n, 100 + n)
         _check(name, desc, w, x, hip_device, "bf16", TOL_V2_BF16)
-        _check(name, desc, w, x, hip_device, "fp32", TOL_FP32, TOL_FP32_KL)
+        _check(name, desc, w, x, hip_device, "bf16x3", TOL_FP32, TOL_FP32_KL)
 
 
 def test_v2_concat_all_layers_batch_invariance(hip_device):
     from galvanise_zero_amd._native import HipNet
     desc = CONCAT_NETS["concat_8x8_se"]
-    for precision in ("bf16", "fp32"):
+    for precision in ("bf16", "bf16x3"):
         net = HipNet(desc, hip_device, precision)
         net.set_weights(to_blob(random_weights(desc, 3, bias_std=0.2, res_gamma=RES_GAMMA)))
         x = random_planes(desc, 300, 9)

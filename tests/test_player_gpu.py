@@ -18,7 +18,7 @@ from test_puct_parity import _player_run
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
 def test_player_batch32_gpu_bit_exact(precision, hip_device):
     setup = Setup("breakthrough")
     setup.desc = BASELINE_CONFIGS[2]["desc"]
@@ -44,7 +44,7 @@ def test_puctplayer_match_on_gpu(hip_device):
                                         think_time=-1, converged_visits=1)
         conf = confs.PUCTPlayerConfig(name="gpu%d" % batch, playouts_per_iteration=playouts, generation="test",
                                       evaluator_config=ev)
-        nn = NeuralNetwork(setup.transformer, HipModel(desc, w, hip_device, "fp32"), None)
+        nn = NeuralNetwork(setup.transformer, HipModel(desc, w, hip_device, "bf16x3"), None)
         return PUCTPlayer(conf, nn=nn, seed=seed)
 
     goals, moves = play_match("breakthroughSmall", [player(32, 200, 3), player(1, 64, 4)])

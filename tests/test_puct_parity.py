@@ -212,6 +212,38 @@ def test_spin_fast_path_identical():
     assert outs[0]["samples"] > 50 and outs[0]["tree_playouts"] > 3 * outs[0]["evaluations"]
 
 
+def test_spin_fast_path_identical_root_latch():
+    """The spin fast path through the root latch (evaluator.cpp:461-475: past 1,000 root visits each
+    reached child draws rng.get() in sorted order and a child holding over 66 % of the traversals is
+    left out when its draw exceeds 0.1).  Deep in a multi-win spin one win often holds the latch; the
+    register loops read that win's draw at its sorted position and discard the others.  A cheap
+    synthetic network takes breakthrough to its deep spins at 400 evals/move; every mode -- fast path
+    off (the reference's loop), on, without register runs, verified, each register loop -- gives
+    identical samples and counters, and the fast path really read latch draws (GZ_SPIN_STATS)."""
+    import subprocess
+    import sys
+    script = os.path.join(os.path.dirname(__file__), "native", "spin_check.py")
+    procs = []
+    for env in ({"GZ_SPIN_FAST": "0"}, {"GZ_SPIN_FAST": "1", "GZ_SPIN_STATS": "1"}, {"GZ_SPIN_FAST": "2"},
+                {"GZ_SPIN_FAST": "1", "GZ_VERIFY_FASTPATH": "1"}, {"GZ_SPIN_FAST": "1", "GZ_SPIN_VEC": "1"},
+                {"GZ_SPIN_FAST": "1", "GZ_SPIN_VEC": "0"}):
+        e = dict(os.environ, **env)
+        procs.append(subprocess.Popen([sys.executable, script, "breakthrough", "8", "8000", "400", "fake"], env=e,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs, errs = [], []
+    for pr in procs:
+        out, err = pr.communicate(timeout=900)
+        assert pr.returncode == 0, err[-2000:]
+        outs.append(json.loads(out.strip().splitlines()[-1]))
+        errs.append(err)
+    assert all(o == outs[0] for o in outs[1:])
+    assert outs[0]["samples"] > 20 and outs[0]["tree_playouts"] > 30 * outs[0]["evaluations"]
+    stats = [ln for ln in errs[1].splitlines() if ln.startswith("gz spin stats:")]
+    assert stats, errs[1][-2000:]
+    fields = dict(kv.split("=") for kv in stats[-1].split(":", 1)[1].split())
+    assert int(fields["latch_draws"]) > 100000, fields
+
+
 def test_player_root_latch_bit_exact():
     """Past 1000 root visits the reference's root latch draws the RNG once per reaching child in
     sorted order (evaluator.cpp:461-475); the engine's unsorted fast path must draw identically."""

@@ -64,7 +64,7 @@ def test_deep_config_runner_matches_oracle(case, hip_device):
     t = setup.transformer
     assert (t.num_channels, t.num_cols, t.num_rows, list(t.policy_dist_count)) == \
         (desc.input_channels, desc.input_columns, desc.input_rows, list(desc.policy_dist_count))
-    net = HipNet(desc, hip_device, "fp32")          # bench.py's arithmetic: bf16x3 split
+    net = HipNet(desc, hip_device, "bf16x3")          # bench.py's arithmetic: bf16x3 split
     net.set_weights(to_blob(random_weights(desc, 7921)))
     conf = _short_game_conf(evals, every_move)
     seed, threads, ppt, spin = 20251019, 2, 2, 1000

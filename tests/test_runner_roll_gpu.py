@@ -37,7 +37,7 @@ def test_generation_roll_live_runner(per_pool, hip_device):
     setup = Setup("breakthrough")
     t = setup.transformer
     wa, wb = to_blob(random_weights(desc, 7921)), to_blob(random_weights(desc, 7922))
-    net = HipNet(desc, hip_device, "fp32")
+    net = HipNet(desc, hip_device, "bf16x3")
     net.set_weights(wa)
     conf = templates.selfplay_config_template()
     conf.evals_per_move = 8
@@ -60,7 +60,7 @@ def test_generation_roll_live_runner(per_pool, hip_device):
     assert all(k > 0 for k in roll["pool_batches"]), roll
     # the net now computes network B exactly (a fresh net with B's weights, bit for bit)
     x = random_planes(desc, 64, 5)
-    fresh = HipNet(desc, hip_device, "fp32")
+    fresh = HipNet(desc, hip_device, "bf16x3")
     fresh.set_weights(wb)
     for a, b in zip(net.forward(x), fresh.forward(x)):
         assert np.array_equal(a, b)
@@ -68,7 +68,7 @@ def test_generation_roll_live_runner(per_pool, hip_device):
         assert st["samples"] > before["samples"]
         return
     # replay one pool through the oracle: A before the roll, B after, filter cleared at the roll
-    neta = HipNet(desc, hip_device, "fp32")
+    neta = HipNet(desc, hip_device, "bf16x3")
     neta.set_weights(wa)
     pool = 5
     mine = [s for s in samples if int(s["match_identifier"].split("_")[1][1:]) == pool]
@@ -109,7 +109,7 @@ def test_roll_timeout_withdraws_and_next_roll_succeeds(hip_device):
     desc = BASELINE_CONFIGS[2]["desc"]
     setup = Setup("breakthrough")
     wa, wb = to_blob(random_weights(desc, 7921)), to_blob(random_weights(desc, 7922))
-    net = HipNet(desc, hip_device, "fp32")
+    net = HipNet(desc, hip_device, "bf16x3")
     net.set_weights(wa)
     conf = templates.selfplay_config_template()
     conf.evals_per_move = 8
@@ -148,7 +148,7 @@ def test_concurrent_rolls_one_owner(hip_device):
     desc = BASELINE_CONFIGS[2]["desc"]
     setup = Setup("breakthrough")
     blobs = [to_blob(random_weights(desc, 7921 + i)) for i in range(3)]
-    net = HipNet(desc, hip_device, "fp32")
+    net = HipNet(desc, hip_device, "bf16x3")
     net.set_weights(blobs[0])
     conf = templates.selfplay_config_template()
     conf.evals_per_move = 8
@@ -159,7 +159,7 @@ def test_concurrent_rolls_one_owner(hip_device):
     x = random_planes(desc, 16, 9)
     refs = []
     for b in blobs:
-        f = HipNet(desc, hip_device, "fp32")
+        f = HipNet(desc, hip_device, "bf16x3")
         f.set_weights(b)
         refs.append(f.forward(x))
     rejected = accepted_both = 0
@@ -211,7 +211,7 @@ def test_runner_recreate_reuses_node_memory(hip_device):
             return int(f.read().split()[1]) * 4096 / 1e9
 
     sm, t, desc = bench.setup_game(2)
-    net = HipNet(desc, hip_device, "fp32")
+    net = HipNet(desc, hip_device, "bf16x3")
     net.set_weights(to_blob(random_weights(desc, 7921)))
     grow = []
     for cycle in range(2):

@@ -33,7 +33,7 @@ NETS = {
 }
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
 @pytest.mark.parametrize("name", sorted(NETS))
 def test_device_roll_image_identical(name, precision, hip_device):
     import torch
@@ -59,6 +59,33 @@ def test_device_roll_image_identical(name, precision, hip_device):
     dev.close()
 
 
+def test_device_roll_orders_after_async_copy(hip_device):
+    """gz_net_set_weights_device needs no caller-side synchronisation: the blob is
+    written by an asynchronous pinned-host copy on torch's current stream, with no
+    torch.cuda.synchronize() before the call (and a large unrelated copy queued ahead of it, so the
+    blob is still in flight when the call starts); the packed image must equal the host path's."""
+    import torch
+    from galvanise_zero_amd._native import HipNet
+    desc = NETS["cfg5"]
+    blob = to_blob(random_weights(desc, 7923))
+    host = HipNet(desc, hip_device, "bf16x3")
+    host.set_weights(blob)
+    dev = HipNet(desc, hip_device, "bf16x3")
+    for _ in range(3):
+        pinned = torch.from_numpy(blob).pin_memory()
+        ballast = torch.empty(1 << 28, dtype=torch.uint8).pin_memory()
+        d_ballast = torch.empty_like(ballast, device="cuda")
+        t = torch.zeros(blob.size, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        d_ballast.copy_(ballast, non_blocking=True)   # 256 MB ahead of the blob on the same stream
+        t.copy_(pinned, non_blocking=True)
+        dev.set_weights_device(t.data_ptr(), t.numel())
+        a, b = host.weight_image(), dev.weight_image()
+        assert np.array_equal(a, b), "%d bytes differ" % np.count_nonzero(a != b)
+    host.close()
+    dev.close()
+
+
 def test_device_roll_faster_than_round_trip(hip_device, monkeypatch):
     """The device fold / pack against the round trip it replaces (D2H copy of the blob, host fold and
     pack, H2D upload; GZ_HOST_WEIGHT_ROLL=1), on amazons' 20 x 256 net (cfg5: 24.9 M parameters)."""
@@ -67,7 +94,7 @@ def test_device_roll_faster_than_round_trip(hip_device, monkeypatch):
     desc = NETS["cfg5"]
     blob = to_blob(random_weights(desc, 7922))
     t = torch.from_numpy(blob).to("cuda")
-    net = HipNet(desc, hip_device, "fp32")
+    net = HipNet(desc, hip_device, "bf16x3")
     times = {}
     for mode in ("device", "round_trip"):
         if mode == "round_trip":

@@ -23,9 +23,9 @@ for n in "$@"; do
   case $n in
     cfg3) timeout -k 10 620 python -u bench.py --config 3 --steps 10 --warmup 2 > $T/bench_cfg3.log 2>&1 || { echo "cfg3 failed"; tail -5 $T/bench_cfg3.log; exit 1; }
           summ $T/bench_cfg3.log ;;
-    len4) timeout -k 10 1150 python -u bench.py --config 4 --pools 1 --batch 1 --age-games 1000 --age-seconds 1000 --steps 2 --warmup 0 --step-rows 16384 --no-cpu-baseline --exit-after-line > $T/len_cfg4.log 2>&1 || { echo "len4 failed"; tail -5 $T/len_cfg4.log; exit 1; }
+    len4) timeout -k 10 1150 python -u bench.py --config 4 --pools 1 --batch 1 --age-games 1000 --age-seconds 1000 --steps 2 --warmup 0 --step-rows 16384 --no-cpu-baseline > $T/len_cfg4.log 2>&1 || { echo "len4 failed"; tail -5 $T/len_cfg4.log; exit 1; }
           summ $T/len_cfg4.log ;;
-    len5) timeout -k 10 1150 python -u bench.py --config 5 --pools 1 --batch 1 --age-games 1000 --age-seconds 1000 --steps 2 --warmup 0 --step-rows 16384 --no-cpu-baseline --exit-after-line > $T/len_cfg5.log 2>&1 || { echo "len5 failed"; tail -5 $T/len_cfg5.log; exit 1; }
+    len5) timeout -k 10 1150 python -u bench.py --config 5 --pools 1 --batch 1 --age-games 1000 --age-seconds 1000 --steps 2 --warmup 0 --step-rows 16384 --no-cpu-baseline > $T/len_cfg5.log 2>&1 || { echo "len5 failed"; tail -5 $T/len_cfg5.log; exit 1; }
           summ $T/len_cfg5.log ;;
   esac
 done
