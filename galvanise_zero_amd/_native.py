@@ -401,6 +401,7 @@ _ENGINE_SIGS = {
     "gz_transformer_to_channels": (ctypes.c_int, [_VP, _U64P, ctypes.POINTER(_U64P), ctypes.c_int, _FP]),
     "gz_supervisor_create": (_VP, [_VP, _VP, ctypes.c_int, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int]),
     "gz_supervisor_destroy": (None, [_VP]),
+    "gz_supervisor_cancel": (ctypes.c_int, [_VP]),
     "gz_supervisor_start_self_play": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.POINTER(GzSelfPlayConfig)]),
     "gz_supervisor_poll": (_FP, [_VP, ctypes.c_int, ctypes.POINTER(_FP), ctypes.c_int, _IP]),
     "gz_supervisor_fetch_samples": (_VP, [_VP]),

@@ -123,6 +123,10 @@ class _CSupervisor(object):
         s = _native.take_string(self.lib.gz_supervisor_fetch_samples(self.handle))
         return json.loads(s) if s else None
 
+    def cancel(self):
+        if self.lib.gz_supervisor_cancel(self.handle) != 0:
+            raise RuntimeError(_native.engine_error())
+
     def add_unique_state(self, state_words):
         s = np.ascontiguousarray(state_words, dtype=np.uint64)
         self.lib.gz_supervisor_add_unique_state(self.handle, s.ctypes.data_as(_U64P))
@@ -337,6 +341,12 @@ class Supervisor(PollerBase):
 
     def clear_unique_states(self):
         self.c_supervisor.clear_unique_states()
+
+    def cancel(self):
+        """Bounded teardown (build extension), callable from another thread: the pools stop at their
+        games' next playout and poll() -- one in progress included -- returns None from then on, so
+        poll_loop() ends."""
+        self.c_supervisor.cancel()
 
     def stats(self):
         return self.c_supervisor.stats()

@@ -293,6 +293,11 @@ extern "C" int gz_supervisor_start_self_play(gz_supervisor* s, int num_workers, 
     })
     return 0;
 }
+extern "C" int gz_supervisor_cancel(gz_supervisor* s) {
+    if (!s) return fail("null supervisor");
+    s->impl->cancel();
+    return 0;
+}
 extern "C" float* gz_supervisor_poll(gz_supervisor* s, int predict_count, float* const* arrays, int num_arrays,
                                      int* buf_count) {
     *buf_count = -1;

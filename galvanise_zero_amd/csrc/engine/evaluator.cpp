@@ -30,6 +30,23 @@ static float puct_log_direct(uint32_t visits) {
     return std::log((1 + visits + cpuct_base_id) / cpuct_base_id);
 }
 
+// Beyond the tables (visits >= 2^26: roots deep in an NN-free spin) the float argument of the log
+// changes only every 8+ visits (float(1 + visits) has that granularity), so the last argument and
+// its log are kept per thread: the same libm call on the same argument, far fewer of them.
+static float puct_log_large(uint32_t visits) {
+    struct Last {
+        float arg = -1.f, val = 0.f;
+    };
+    static thread_local Last last;
+    const float cpuct_base_id = 19652.0f;
+    const float arg = (1 + visits + cpuct_base_id) / cpuct_base_id;
+    if (arg != last.arg) {
+        last.arg = arg;
+        last.val = std::log(arg);
+    }
+    return last.val;
+}
+
 namespace {
 constexpr int kPuctLogBlockBits = 16, kPuctLogBlocks = 1024;   // visits < 2^26
 std::atomic<float*> g_puct_log[kPuctLogBlocks];
@@ -50,7 +67,7 @@ __attribute__((noinline)) float* puct_log_block(uint32_t b) {
 
 static inline float puct_log(uint32_t visits) {
     const uint32_t b = visits >> kPuctLogBlockBits;
-    if (b >= (uint32_t)kPuctLogBlocks) return puct_log_direct(visits);
+    if (b >= (uint32_t)kPuctLogBlocks) return puct_log_large(visits);
     float* t = g_puct_log[b].load(std::memory_order_acquire);
     if (__builtin_expect(t == nullptr, 0)) t = puct_log_block(b);
     return t[visits & ((1u << kPuctLogBlockBits) - 1)];
@@ -63,7 +80,7 @@ struct PuctLogCursor {
     inline float at(uint32_t visits) {
         const uint32_t vb = visits >> kPuctLogBlockBits;
         if (__builtin_expect(vb != b, 0)) {
-            if (vb >= (uint32_t)kPuctLogBlocks) return puct_log_direct(visits);
+            if (vb >= (uint32_t)kPuctLogBlocks) return puct_log_large(visits);
             t = g_puct_log[vb].load(std::memory_order_acquire);
             if (t == nullptr) t = puct_log_block(vb);
             b = vb;
@@ -114,6 +131,13 @@ struct SpinStats {
     }
 };
 SpinStats g_spin_stats;
+inline int spin_dump_at() {
+    static const int v = [] {
+        const char* e = std::getenv("GZ_SPIN_DUMP");
+        return e != nullptr ? std::atoi(e) : -1;
+    }();
+    return v;
+}
 inline void sd(SpinStat i, long n = 1) {
     if (__builtin_expect(g_spin_stats.on, 0)) g_spin_stats.c[i].fetch_add(n, std::memory_order_relaxed);
 }
@@ -2474,6 +2498,38 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
             depth = treePlayout(root, path);
             ran = 1;
             sd(kSdOrdinaryPlayouts);
+            if (__builtin_expect(g_spin_stats.on, 0) && stats.num_evaluations == ev0 &&
+                stats.num_tree_playouts - stats.num_evaluations == spin_dump_at()) {
+                // diagnostics (GZ_SPIN_DUMP=<n>): the root and the last playout's path once a move
+                // has run n NN-free playouts (at most 6 dumps per process)
+                static std::atomic<int> dumps{0};
+                if (dumps.fetch_add(1) < 6) {
+                    const int lead = root->lead_role_index;
+                    std::fprintf(stderr, "gz spin dump: depth %d root visits %u lead %d score %.6f evals %d playouts %d\n",
+                                 root->game_depth, root->visits, lead, root->getCurrentScore(lead < 0 ? 0 : lead),
+                                 stats.num_evaluations, stats.num_tree_playouts);
+                    for (int i = 0; i < root->num_children; ++i) {
+                        const PuctNodeChild* c = root->getNodeChild(0, i);
+                        const PuctNode* cn = c->to_node;
+                        std::fprintf(stderr, "  child %2d trav %9u pol %.4f", i, c->traversals, c->policy_prob);
+                        if (cn)
+                            std::fprintf(stderr, " visits %9u score %.6f fin %d nch %d term %d\n", cn->visits,
+                                         cn->getCurrentScore(lead), (int)cn->is_finalised, cn->num_children,
+                                         (int)cn->isTerminal());
+                        else
+                            std::fprintf(stderr, " unexpanded\n");
+                    }
+                    for (size_t k = 0; k < path.size(); ++k) {
+                        const PuctNode* n = path[k].node;
+                        const int l = n->lead_role_index;
+                        int ci = -1;
+                        for (int i = 0; i < n->num_children && path[k].choice; ++i)
+                            if (n->getNodeChild(0, i) == path[k].choice) ci = i;
+                        std::fprintf(stderr, "  path %zu: lead %d visits %u score(lead) %.6f fin %d nch %d -> child %d\n", k, l,
+                                     n->visits, n->getCurrentScore(l < 0 ? 0 : l), (int)n->is_finalised, n->num_children, ci);
+                    }
+                }
+            }
             if (__builtin_expect(g_spin_stats.on, 0) && stats.num_evaluations == ev0) {
                 int nw = 0;
                 for (int i = 0; i < root->num_children; ++i) {

@@ -78,8 +78,19 @@ void Supervisor::createWorkers(const SelfPlayConfig* config_in) {
 }
 
 // supervisor.cpp:101-168
+void Supervisor::cancel() {
+    cancelled.store(true);
+    for (SelfPlayManager* m : all_managers) m->cancel();
+    {
+        std::lock_guard<std::mutex> lk(ready_m);
+        ready_flag++;
+    }
+    ready_cv.notify_all();
+}
+
 const ReadyEvent* Supervisor::poll(int predict_count, const std::vector<float*>& data) {
     GZ_ASSERT(0 <= predict_count && predict_count <= batch_size);
+    if (cancelled.load()) return &cancelled_event;
 
     auto populateEvent = [&](SelfPlayManager* manager) {
         PredictDoneEvent* event = manager->getPredictDoneEvent();
@@ -126,6 +137,7 @@ const ReadyEvent* Supervisor::poll(int predict_count, const std::vector<float*>&
             }
         }
         if (in_progress_worker != nullptr) break;
+        if (cancelled.load()) return &cancelled_event;
         std::unique_lock<std::mutex> lk(ready_m);
         ready_cv.wait(lk, [&] { return ready_flag != seen; });
     }

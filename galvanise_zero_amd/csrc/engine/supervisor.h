@@ -91,6 +91,9 @@ public:
     void setSampleInterval(int n) { sample_interval = n < 1 ? 1 : n; }
     void clearUniqueStates();
     PoolStats stats();
+    // Bounded teardown (any thread, also while another thread is inside poll()): every pool is
+    // cancelled (NetworkScheduler::cancel) and poll() returns an empty batch from then on.
+    void cancel();
 
     // called by workers when a pool is ready
     void notifyReady() {
@@ -115,6 +118,8 @@ private:
     int sample_interval = 1024;
     long next_game_index = 0;
 
+    std::atomic<bool> cancelled{false};
+    ReadyEvent cancelled_event;        // the empty batch poll() returns once cancelled
     SelfPlayManager* inline_sp_manager = nullptr;
     SelfPlayManager* in_progress_manager = nullptr;
     SelfPlayWorker* in_progress_worker = nullptr;

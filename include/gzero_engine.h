@@ -163,6 +163,10 @@ int gz_supervisor_start_self_play(gz_supervisor* s, int num_workers, const gz_se
  * [predict_count*V]; returns the engine-owned planes buffer and *buf_count floats (valid until the
  * next poll); NULL with *buf_count 0 when finished, NULL with *buf_count -1 on error. */
 float* gz_supervisor_poll(gz_supervisor* s, int predict_count, float* const* arrays, int num_arrays, int* buf_count);
+/* Bounded teardown from any thread (build extension; the reference ends its workers with the
+ * process): every pool is cancelled (gz_pool_cancel) and gz_supervisor_poll -- one in progress
+ * included -- returns NULL with *buf_count 0 from then on. */
+int gz_supervisor_cancel(gz_supervisor* s);
 /* fetch_samples: JSON list of Sample dicts (datadesc.py:8-38 / sampleToDict supervisor_impl.cpp:75-118)
  * or NULL when there are none; free with gz_free. */
 char* gz_supervisor_fetch_samples(gz_supervisor* s);

@@ -111,3 +111,85 @@ def test_deep_config_runner_matches_oracle(case, hip_device):
     print("%s: %d samples of 2 pools identical to the oracle (%d-block x %d net, %d evals per move)" % (
         case, checked, desc.residual_layers, desc.cnn_filter_size, evals))
     assert checked >= need
+
+
+
+def _every_move_conf(evals):
+    """The self-play template (resignation possible in 1 % of games, run-to-end at 32 evaluations) at
+    `evals` evaluations per move with every move sampled: complete games, whose samples appear at
+    the game's end (selfplay.cpp:296-337), not opening-only resigns."""
+    conf = templates.selfplay_config_template()
+    conf.evals_per_move = evals
+    conf.oscillate_sampling_pct = 1.0
+    return conf
+
+
+# case: (config, game, games in the pool, evals per move); both games must complete with >= 20
+# samples each
+CASES_200 = {"reversi_cfg3_200": (3, "reversi", 2, 200),
+             "hexLG13_cfg4_200": (4, "hexLG13", 2, 200),
+             "amazons_cfg5_200": (5, "amazons_10x10", 2, 200)}
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("case", list(CASES_200))
+def test_deep_config_runner_matches_oracle_200(case, hip_device):
+    """cfg3-5's games through the native runner on their full bench nets (bf16x3) at 200 evaluations
+    per move, played to the end: the pool replayed through the oracle with the same HIP forward,
+    every sample identical, >= 20 per game (the endgame's spins, terminal wins and draws included)."""
+    import time
+    from galvanise_zero_amd._native import HipNet
+    from galvanise_zero_amd.runner import SelfPlayRunner
+    from oracle import puct_ref as P
+    cfg, game, B, evals = CASES_200[case]
+    desc = BASELINE_CONFIGS[cfg]["desc"]
+    setup = Setup(game, draw_head=(game == "reversi"))
+    t = setup.transformer
+    assert (t.num_channels, t.num_cols, t.num_rows, list(t.policy_dist_count), t.num_rewards) == \
+        (desc.input_channels, desc.input_columns, desc.input_rows, list(desc.policy_dist_count), desc.num_values)
+    net = HipNet(desc, hip_device, "bf16x3")
+    net.set_weights(to_blob(random_weights(desc, 7921)))
+    conf = _every_move_conf(evals)
+    seed, spin = 20251020, 1000
+    r = SelfPlayRunner(net, setup.sm, t, conf, device=hip_device, num_threads=1, pools_per_thread=1,
+                       batch_size=B, seed=seed, keep_samples=True, spin_yield_playouts=spin,
+                       min_launch_rows=1, max_launch_wait_us=0)
+    r.start()
+    t0 = time.time()
+    while r.stats()["games_completed"] < B and time.time() - t0 < 500:
+        time.sleep(1)
+    r.stop()
+    st = r.stats()
+    samples = r.fetch_samples()
+    r.close()
+    per_game = {}
+    for s in samples:
+        per_game[s["match_identifier"]] = per_game.get(s["match_identifier"], 0) + 1
+    print(case, "runner", {k: st[k] for k in ("games_completed", "rows", "tree_playouts")}, "samples per game",
+          per_game, "%.0f s" % (time.time() - t0), flush=True)
+    assert st["games_completed"] >= B, st
+    d = attr.asdict(conf)
+    for k in ("puct_config", "run_to_end_puct_config"):
+        d[k]["spin_yield_playouts"] = spin
+    man = P.Manager(setup.ref_sm, setup.ref_planes, B, P.UniqueStates(setup.ref_planes.hash_mask(), 1000),
+                    "t", seed, 0, list(t.policy_dist_count), t.num_rewards, setup.num_prev_states)
+    man.start(d)
+    pred = (0, [np.zeros(0, np.float32)] * setup.sm.role_count, np.zeros(0, np.float32))
+    it = 0
+    while len(man.samples) < len(samples):
+        if it % 2000 == 0:
+            print("oracle poll %d: %d/%d samples" % (it, len(man.samples), len(samples)), flush=True)
+        buf = man.poll(*pred)
+        assert buf is not None
+        x = buf.reshape(-1, t.num_channels, t.num_cols, t.num_rows)
+        outs = net.forward(x)
+        pred = (x.shape[0], outs[:-1], outs[-1])
+        it += 1
+    n = len(samples)
+    got = [sample_key(setup, _suffix(s), True) for s in samples]
+    exp = [sample_key(setup, _suffix(s), False) for s in man.samples[:n]]
+    assert got == exp
+    done = sorted(per_game.values(), reverse=True)[:B]
+    assert len(done) == B and min(done) >= 20, per_game
+    print("%s: %d samples identical to the oracle, %s per game (%d-block x %d net, %d evals per move)" % (
+        case, n, done, desc.residual_layers, desc.cnn_filter_size, evals))

@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--logit-scale", type=float, default=3.0)
     ap.add_argument("--report", type=float, default=10)
     a = ap.parse_args()
+    if os.environ.get("GZ_SPROF_LIB"):   # host sampling profiler (tools/sprof), as bench.py loads it
+        import ctypes
+        ctypes.CDLL(os.environ["GZ_SPROF_LIB"])
     import bench
     from galvanise_zero_amd import cppinterface
     from galvanise_zero_amd.nn.desc import BASELINE_CONFIGS
@@ -62,8 +65,13 @@ def main():
     t0 = time.time()
     last = t0
     prev = sup.stats()
+    # a poll can block for minutes while every pool spins: a timer cancels the supervisor at the end
+    import threading
+    timer = threading.Timer(a.seconds, sup.cancel)
+    timer.start()
     while time.time() - t0 < a.seconds:
-        sup.poll(do_stats=True)
+        if sup.poll(do_stats=True) is None:
+            break
         if time.time() - last >= a.report:
             st = sup.stats()
             rows = st["evaluations"] - prev["evaluations"]
@@ -77,6 +85,8 @@ def main():
     print("total: %.0f leaf-evals/s, NN-free/leaf %.1f, games %d" % (
         st["evaluations"] / (time.time() - t0), (st["tree_playouts"] - st["evaluations"]) / max(1, st["evaluations"]),
         st["games_completed"]), flush=True)
+    timer.cancel()
+    sup.cancel()
     t = time.time()
     del sup   # bounded teardown: the workers' pools are cancelled (gz_pool_cancel)
     print("teardown %.2f s" % (time.time() - t), flush=True)

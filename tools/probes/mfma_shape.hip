@@ -14,6 +14,8 @@
 //   s24: s20 with the weights staged through an LDS ring by LDS-DMA (global_load_lds_dwordx4)
 //   s25 / s26: s20 with the waves split 2 x 2 (co half x board): twice the weight loads, half the
 //        B reads per k-step; ring 4 / 2
+//   s33 / s34: s32 with the B fragments one k-step ahead (s17's scheme), weights in registers /
+//        streamed through a 4-k-step ring (s20's)
 // Same FLOPs, same LDS bytes, same accumulator registers (64), one workgroup of 4 waves per CU (the
 // LDS allocation), every CU busy, random data (the clock the chip holds depends on it:
 // MI355X_MICROARCH.md DVFS item 7).  Reports wall time, the in-kernel cycles (s_memtime) and the
@@ -345,6 +347,72 @@ __global__ void __launch_bounds__(256) probe(const bf16x8* __restrict__ wsrc, fl
         for (int c = 0; c < 4; ++c)
 #pragma unroll
             for (int t = 0; t < 4; ++t) sum += acc[c][t][0] + acc[c][t][1] + acc[c][t][2] + acc[c][t][3];
+    } else if constexpr (SHAPE == 33 || SHAPE == 34) {
+        // s32 with the B fragments read one k-step ahead into a second register set (VERDICT r5 item
+        // 2: the like-for-like comparison with s17 / s20); s33 the weights in registers, s34 streamed
+        // from the 7 MB image through a 4-k-step register ring (1 KB contiguous wave-loads, as s20)
+        constexpr int D = 4, NSTEP = 448;
+        f32x16 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) asm volatile("" : "+a"(acc[t]));
+        asm volatile("s_nop 1" ::: "memory");
+        const int li = lane & 31, h = lane >> 5;
+        const bf16x8* wimg = wsrc + 16 * 256 * 8 / 8;
+        auto wl_at = [&](int j, int f) { return wimg[((size_t)(j % NSTEP) * 4 + f) * 256 + tid]; };
+        bf16x8 ring[D][4];
+        if constexpr (SHAPE == 34) {
+#pragma unroll
+            for (int d = 0; d < D - 1; ++d)
+#pragma unroll
+                for (int f = 0; f < 4; ++f) ring[d][f] = wl_at(d, f);
+        }
+        bf16x8 b[2][4][2][2];   // [set][position tile][k half][hi / lo]
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh) {
+                const char* a = lds + (32 * t + li) * kRowBytes + 16 * (2 * kh + h);
+                b[0][t][kh][0] = *(const bf16x8*)a;
+                b[0][t][kh][1] = *(const bf16x8*)(a + 256);
+            }
+        for (int k = 0; k < ksteps; k += 4) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int j = k + s;
+                if constexpr (SHAPE == 34) {
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) ring[(s + D - 1) % D][f] = wl_at(j + D - 1, f);
+                }
+                const int kn = (j + 1) & 3;
+                const int cb = s & 1, nb = cb ^ 1;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+#pragma unroll
+                    for (int kh = 0; kh < 2; ++kh) {
+                        if constexpr (SHAPE == 34)
+                            chain32(acc[t], ring[s][2 * kh], b[cb][t][kh][0], b[cb][t][kh][1], ring[s][2 * kh + 1]);
+                        else
+                            chain32(acc[t], wh[s][kh], b[cb][t][kh][0], b[cb][t][kh][1], wl[s][kh]);
+                    }
+#pragma unroll
+                    for (int kh = 0; kh < 2; ++kh) {
+                        const char* a = lds + (32 * t + li) * kRowBytes + 16 * (4 * kn + 2 * kh + h) % 256;
+                        b[nb][t][kh][0] = *(const bf16x8*)a;
+                        b[nb][t][kh][1] = *(const bf16x8*)(a + 256);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sum += acc[t][r];
     } else {
         f32x16 acc[4];
 #pragma unroll
@@ -386,6 +454,16 @@ int main(int argc, char** argv) {
     const int ksteps = argc > 1 ? std::atoi(argv[1]) : 2048;
     const int grid = argc > 2 ? std::atoi(argv[2]) : 256 * 4;
     const int reps = argc > 3 ? std::atoi(argv[3]) : 30;
+    // shapes to run (argv[4], comma-separated; default the round-6 like-for-like set)
+    std::vector<int> shapes;
+    {
+        const char* list = argc > 4 ? argv[4] : "16,17,20,32,33,34";
+        for (const char* q = list; *q;) {
+            shapes.push_back(std::atoi(q));
+            while (*q && *q != ',') ++q;
+            if (*q == ',') ++q;
+        }
+    }
     // the register weights (16 x 256 fragments), then the 7 MB streamed weight image (448 k-steps x 4 x 256)
     std::vector<unsigned short> hw((size_t)(16 * 256 + 448 * 4 * 256) * 8);
     unsigned x = 12345;
@@ -411,6 +489,8 @@ int main(int argc, char** argv) {
     CHK(hipFuncSetAttribute((const void*)probe<24>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
     CHK(hipFuncSetAttribute((const void*)probe<25>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
     CHK(hipFuncSetAttribute((const void*)probe<26>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<33>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
+    CHK(hipFuncSetAttribute((const void*)probe<34>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds));
     hipEvent_t e0, e1;
     CHK(hipEventCreate(&e0));
     CHK(hipEventCreate(&e1));
@@ -418,7 +498,7 @@ int main(int argc, char** argv) {
     const double flops = (double)grid * 4 * ksteps * 2.0 * 32 * 128 * 32;
     std::vector<unsigned long long> cyc(grid);
     for (int round = 0; round < 3; ++round)
-        for (int shape : {17, 20, 25, 26}) {
+        for (int shape : shapes) {
             auto launch = [&]() {
                 if (shape == 16) probe<16><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else if (shape == 17) probe<17><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
@@ -430,6 +510,8 @@ int main(int argc, char** argv) {
                 else if (shape == 24) probe<24><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else if (shape == 25) probe<25><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else if (shape == 26) probe<26><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 33) probe<33><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
+                else if (shape == 34) probe<34><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
                 else probe<32><<<grid, 256, kLds>>>(dw, dout, dcyc, ksteps);
             };
             for (int i = 0; i < 3; ++i) launch();   // warm (and let the clock settle)
