@@ -7,6 +7,8 @@
 #include "tls.h"
 #include "transformer.h"
 
+#include <x86intrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -31,20 +33,25 @@ static float puct_log_direct(uint32_t visits) {
 }
 
 // Beyond the tables (visits >= 2^26: roots deep in an NN-free spin) the float argument of the log
-// changes only every 8+ visits (float(1 + visits) has that granularity), so the last argument and
-// its log are kept per thread: the same libm call on the same argument, far fewer of them.
-static float puct_log_large(uint32_t visits) {
-    struct Last {
-        float arg = -1.f, val = 0.f;
-    };
-    static thread_local Last last;
+// changes only every 8+ visits (float(1 + visits) has that granularity): a small direct-mapped
+// cache of (argument, log) pairs, each one 64-bit word (a racing store is a whole pair), keyed by
+// the argument's bits -- the same libm call on the same argument, far fewer of them.
+static inline float puct_log_arg(uint32_t visits) {
     const float cpuct_base_id = 19652.0f;
-    const float arg = (1 + visits + cpuct_base_id) / cpuct_base_id;
-    if (arg != last.arg) {
-        last.arg = arg;
-        last.val = std::log(arg);
-    }
-    return last.val;
+    return (1 + visits + cpuct_base_id) / cpuct_base_id;
+}
+namespace {
+std::atomic<uint64_t> g_large_log[1024];
+}
+static float puct_log_large(uint32_t visits) {
+    const float arg = puct_log_arg(visits);
+    const uint32_t a = __builtin_bit_cast(uint32_t, arg);
+    std::atomic<uint64_t>& e = g_large_log[(a >> 3) & 1023];
+    const uint64_t w = e.load(std::memory_order_relaxed);
+    if ((uint32_t)(w >> 32) == a && w != 0) return __builtin_bit_cast(float, (uint32_t)w);
+    const float v = std::log(arg);
+    e.store((uint64_t)a << 32 | __builtin_bit_cast(uint32_t, v), std::memory_order_relaxed);
+    return v;
 }
 
 namespace {
@@ -73,14 +80,23 @@ static inline float puct_log(uint32_t visits) {
     return t[visits & ((1u << kPuctLogBlockBits) - 1)];
 }
 
-// puct_log at consecutive visit counts (a spin run): the current 64K block held, refreshed at its end
+// puct_log at consecutive visit counts (a spin run): the current 64K block held, refreshed at its end;
+// beyond the tables the last argument and its log
 struct PuctLogCursor {
     const float* t = nullptr;
     uint32_t b = ~0u;
+    float last_arg = -1.f, last_val = 0.f;
     inline float at(uint32_t visits) {
         const uint32_t vb = visits >> kPuctLogBlockBits;
         if (__builtin_expect(vb != b, 0)) {
-            if (vb >= (uint32_t)kPuctLogBlocks) return puct_log_large(visits);
+            if (vb >= (uint32_t)kPuctLogBlocks) {
+                const float arg = puct_log_arg(visits);
+                if (arg != last_arg) {
+                    last_arg = arg;
+                    last_val = puct_log_large(visits);
+                }
+                return last_val;
+            }
             t = g_puct_log[vb].load(std::memory_order_acquire);
             if (t == nullptr) t = puct_log_block(vb);
             b = vb;
@@ -109,6 +125,9 @@ enum SpinStat {
     // register runs: how they end
     kSdRegRuns, kSdRegFailNoise, kSdRegFailLatch, kSdRegFailSep, kSdRegExpired,
     kSdLatchDraws,   // fast-path playouts that read a root-latch draw
+    kSdCycSpin, kSdCycFree, kSdCycEval,   // TSC cycles in spin runs / NN-free / evaluating ordinary playouts
+    kSdFreeLine,     // NN-free ordinary playouts whose path below the root is forced (1 child / forced win)
+    kSdSelectForced, // selections decided by the forced-reply pass
     kSdCount
 };
 struct SpinStats {
@@ -124,7 +143,8 @@ struct SpinStats {
             "free_d3_forced_win",
             "exit_finalised", "exit_conv_playouts", "exit_conv_evals", "exit_nonconv_evals", "exit_other",
             "free_at_conv_playouts", "free_at_conv_evals", "free_at_nonconv_evals",
-            "reg_runs", "reg_fail_noise", "reg_fail_latch", "reg_fail_sep", "reg_expired", "latch_draws"};
+            "reg_runs", "reg_fail_noise", "reg_fail_latch", "reg_fail_sep", "reg_expired", "latch_draws",
+            "cyc_spin", "cyc_free", "cyc_eval", "free_line", "select_forced"};
         std::fprintf(stderr, "gz spin stats:");
         for (int i = 0; i < kSdCount; ++i) std::fprintf(stderr, " %s=%ld", names[i], c[i].load());
         std::fprintf(stderr, "\n");
@@ -762,6 +782,50 @@ PuctNodeChild* PuctEvaluator::selectChild(PuctNode* node, Path& path) {
 
     const double sqrt_node_visits = std::sqrt(node->visits + 1);
     const int n = node->num_children;
+
+    // Forced reply (depth > 0): the reference returns the first finalised child scoring > 0.99 for
+    // the node's lead role in sortedChildrenSelect order (evaluator.cpp:415-424); with a unique
+    // highest-scoring such child, no tie among them and no RNG draw before it (the inflight
+    // discount, :441-444), that child is the result whatever else the node holds.  Deep in an
+    // NN-free spin (a solved endgame: every playout a forced line to a terminal) this is the common
+    // interior node: one light pass over the mirrors instead of the full selection pass.
+    if (depth > 0 && mirror_ok && n <= 65535) {
+        const PuctNodeChild* cs0 = node->children();
+        int fw = -1;
+        float fk = 0.f;
+        bool tied = false, draws = false;
+        for (int i = 0; i < n; ++i) {
+            const PuctNodeChild* c = cs0 + i;
+            if (c->to_node == nullptr || c->unselectable) continue;
+            if (c->m_inflight != 0 && c->traversals > 0) draws = true;
+            if ((c->m_flags & (kMirrorFinalised | kMirrorAllUnselectable)) != kMirrorFinalised) continue;
+            const float k = c->m_score;
+            if (!((double)k > 0.99)) continue;
+            if (fw < 0 || k > fk) {
+                fw = i;
+                fk = k;
+                tied = false;
+            } else if (k == fk) {
+                tied = true;
+            }
+        }
+        if (fw >= 0 && !tied && !draws) {
+            PuctNodeChild* chosen = node->getNodeChild(0, fw);
+            if (verify_fastpath()) {
+                const Rng rng_before = rng;
+                PuctNodeChild* lit_best = nullptr;
+                PuctNodeChild* lit = selectChildLiteral(node, depth, priorScore(node, depth), sqrt_node_visits, &lit_best);
+                if (lit != chosen || !(rng == rng_before)) {
+                    std::fprintf(stderr, "gz forced-reply verification mismatch (depth %d, n %d)\n", depth, n);
+                    std::abort();
+                }
+                count_verified();
+            }
+            sd(kSdSelectForced);
+            path.emplace_back(node, chosen, chosen);
+            return chosen;
+        }
+    }
     if (n > 65535) {
         PuctNodeChild* best = nullptr;
         PuctNodeChild* chosen = selectChildLiteral(node, depth, priorScore(node, depth), sqrt_node_visits, &best);
@@ -2490,12 +2554,17 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
         int limit = 1 << 20;
         if (conf->spin_yield_playouts > 0) limit = conf->spin_yield_playouts - quiet_playouts;
         int depth = 2;
+        const uint64_t c0 = __builtin_expect(g_spin_stats.on, 0) ? __rdtsc() : 0;
         int ran = spinRun(limit, multi);
+        if (__builtin_expect(g_spin_stats.on, 0) && ran > 0) sd(kSdCycSpin, (long)(__rdtsc() - c0));
         if (ran == 0) {
             spin.valid = false;
             path.clear();
             const int ev0 = stats.num_evaluations;
+            const uint64_t c1 = __builtin_expect(g_spin_stats.on, 0) ? __rdtsc() : 0;
             depth = treePlayout(root, path);
+            if (__builtin_expect(g_spin_stats.on, 0))
+                sd(stats.num_evaluations == ev0 ? kSdCycFree : kSdCycEval, (long)(__rdtsc() - c1));
             ran = 1;
             sd(kSdOrdinaryPlayouts);
             if (__builtin_expect(g_spin_stats.on, 0) && stats.num_evaluations == ev0 &&
@@ -2542,6 +2611,15 @@ void PuctEvaluator::playoutMain(int max_evaluations, double end_time) {
                     path[2].node->getCurrentScore(path[1].node->lead_role_index) > 0.99)
                     sd(kSdFreeX1Win);
                 if (convergedExact(conf->converged_visits)) sd(kSdFreeConv);
+                bool line = true;
+                for (size_t k = 1; k + 1 < path.size() && line; ++k) {
+                    const PuctNode* pn = path[k].node;
+                    const PuctNodeChild* pc = path[k].choice;
+                    line = pn->num_children == 1 ||
+                           (pc && pc->to_node && pc->to_node->is_finalised && pn->lead_role_index >= 0 &&
+                            pc->to_node->getCurrentScore(pn->lead_role_index) > 0.99);
+                }
+                if (line) sd(kSdFreeLine);
             }
         }
         stats.playouts_max_depth = std::max(depth, stats.playouts_max_depth);

@@ -82,9 +82,10 @@ def main():
                 flush=True)
             prev, last = st, time.time()
     st = sup.stats()
-    print("total: %.0f leaf-evals/s, NN-free/leaf %.1f, games %d" % (
-        st["evaluations"] / (time.time() - t0), (st["tree_playouts"] - st["evaluations"]) / max(1, st["evaluations"]),
-        st["games_completed"]), flush=True)
+    el = time.time() - t0
+    print("total: %.0f leaf-evals/s, %.2f M tree playouts/s, NN-free/leaf %.1f, games %d" % (
+        st["evaluations"] / el, st["tree_playouts"] / el / 1e6,
+        (st["tree_playouts"] - st["evaluations"]) / max(1, st["evaluations"]), st["games_completed"]), flush=True)
     timer.cancel()
     sup.cancel()
     t = time.time()
