@@ -144,6 +144,21 @@ private:
     SpinEpoch spin;
     Path spin_path;
 
+    // Forced replies among tied finalised wins (selectChild): the reference returns the first of
+    // them in sortedChildrenSelect order, which std::sort's permutation of all the node's keys
+    // decides.  While every visit to the node since goes through that child, no other child is
+    // touched (single-parent trees: mirror_ok), every key is unchanged, and so is the answer: an
+    // entry holds (node, its visits and the child's traversals then) and is valid exactly while
+    // the node's visits and the child's traversals grew alike.  Entries of freed nodes are cleared.
+    struct ForcedEntry {
+        const PuctNode* node = nullptr;
+        uint32_t visits = 0, trav = 0;
+        uint16_t child = 0, nch = 0;
+    };
+    static constexpr int kForcedSlots = 64;
+    ForcedEntry forced_cache[kForcedSlots];
+    static int forcedSlot(const PuctNode* n) { return (int)((reinterpret_cast<uintptr_t>(n) >> 6) % kForcedSlots); }
+
     struct MaskedKey {
         std::vector<uint64_t> w;
         bool operator==(const MaskedKey& o) const { return w == o.w; }
