@@ -625,7 +625,8 @@ def main():
         print(json.dumps(out), flush=True)
     t_stop = time.time()
     runner.stop()
-    out["runner_stop_s"] = time.time() - t_stop
+    if rank == 0:   # (only rank 0 builds the line)
+        out["runner_stop_s"] = time.time() - t_stop
     runner.close()   # frees the games' trees before the CPU baseline
     if rank == 0 and not line_first:
         out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds, evals, args.mode, args.batch, args.config)
