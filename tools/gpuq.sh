@@ -3,6 +3,6 @@
 OUT=$1; shift
 for i in 1 2 3 4 5 6 7 8; do
   /usr/local/graft/bin/gpurun "$@" > $OUT 2>&1
-  if grep -q "nothing was charged\|no free box right now" $OUT && ! grep -q "status=ok\|status=fail" $OUT; then sleep 150; continue; fi
+  if grep -q "nothing was charged\|no free box right now\|while being prepared; retry\|backing off" $OUT && ! grep -q "status=ok\|status=fail" $OUT; then sleep 150; continue; fi
   break
 done
