@@ -108,3 +108,22 @@ def test_two_rank_sharding_matches_single_process():
     assert len(single) > 0
     assert sharded == single
     assert stats["evaluations"] == sum(r["evaluations"] for r in ranks)
+
+
+def test_renewal_games_per_sec_aggregates_ranks():
+    """bench.per_game_cost's renewal games/s: the rate it is given is per rank, so the
+    reported value is world x the per-rank figure (each rank runs the same workload on its own game
+    range); the per-rank figure is reported beside it."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    K = 8
+    o = {"games": [0] * K, "evals": [0] * K, "tree_playouts": [0] * K, "moves": [0] * K, "spin_epochs": [0] * K,
+         "engine_s": [0.0] * K, "cost_hist": [0] * 16, "inflight_games": 4, "inflight_engine_s": 2.0,
+         "inflight_evals": 4000, "inflight_games_ord": [4] + [0] * (K - 1),
+         "inflight_engine_s_ord": [2.0] + [0.0] * (K - 1), "inflight_evals_ord": [4000] + [0] * (K - 1)}
+    one = bench.per_game_cost(o, threads=2, slots=4, run_s=10.0, rate=1000.0, world=1)
+    two = bench.per_game_cost(o, threads=2, slots=4, run_s=10.0, rate=1000.0, world=2)
+    r1, r2 = one["first_game_cohort"]["games_per_sec_renewal"], two["first_game_cohort"]["games_per_sec_renewal"]
+    assert r1["value"] == r1["per_rank"] == 1000.0 / 1000.0
+    assert r2["value"] == 2 * r2["per_rank"] and r2["ranks"] == 2
