@@ -125,9 +125,9 @@ def _every_move_conf(evals):
 
 
 # case: (config, game, games in the pool, evals per move); every game must complete with >= 20
-# samples.  hexLG13's and amazons' complete games take the Python oracle 5-15 minutes to replay
-# (10-20 ms of tree work per evaluation for their 169-cell / 2,000-move positions): they run with
-# GZ_LONG_TESTS=1 (their logs: profiles/r06g_replay_*.log); reversi runs in every -m gpu pass.
+# samples.  hexLG13's and amazons' complete games take minutes each (amazons: 3.3 min on MI355X,
+# a 160-move game; the Python oracle's tree work per evaluation dominates): they run with
+# GZ_LONG_TESTS=1 (their logs: profiles/r06g*_replay_*.log); reversi runs in every -m gpu pass.
 CASES_200 = {"reversi_cfg3_200": (3, "reversi", 2, 200),
              "hexLG13_cfg4_200": (4, "hexLG13", 1, 200),
              "amazons_cfg5_200": (5, "amazons_10x10", 1, 200)}
