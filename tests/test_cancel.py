@@ -32,3 +32,55 @@ def test_pool_cancel_bounds_a_spinning_poll():
     assert not st["alive"] and st["cancel_to_return_s"] < 1.0, st
     assert st["rows_after_cancel"] == [0, 0, 0], st       # every later poll returns at once, empty
     assert st["destroy_s"] < 1.0, st
+
+
+@pytest.mark.timeout(300)
+def test_supervisor_cancel_ends_poll_loop():
+    """cppinterface.Supervisor.cancel() (gz_supervisor_cancel) from another thread ends a
+    poll_loop() whose worker pools are busy -- the reference's Supervisor has no such call (its
+    workers end with the process) -- and the supervisor tears down promptly afterwards."""
+    import threading
+    import time
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests", "native"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from galvanise_zero_amd import cppinterface
+    from galvanise_zero_amd.defs import templates
+    from puct_harness import Setup
+    from spin_check import fake_forward
+    setup = Setup("breakthrough")
+
+    class Model(object):
+        def predict_on_batch(self, x):
+            return fake_forward(setup.desc, np.asarray(x, dtype=np.float32))
+
+    class NN(object):
+        gdl_bases_transformer = setup.transformer
+
+        def get_model(self):
+            return Model()
+
+    conf = templates.selfplay_config_template()
+    conf.evals_per_move = 400
+    sup = cppinterface.Supervisor(setup.sm, NN(), batch_size=8, seed=2, per_pool_unique_states=True)
+    sup.start_self_play(conf, 2)
+    done = {}
+
+    def loop():
+        sup.poll_loop()
+        done["t"] = time.time()
+
+    th = threading.Thread(target=loop, daemon=True)
+    th.start()
+    time.sleep(5.0)
+    assert th.is_alive()                          # self-play runs forever until cancelled
+    t0 = time.time()
+    sup.cancel()
+    th.join(timeout=30)
+    assert not th.is_alive() and done["t"] - t0 < 2.0, done
+    assert sup.poll() is None                     # every later poll returns at once, empty
+    st = sup.stats()
+    assert st["evaluations"] > 0, st
+    t1 = time.time()
+    del sup
+    assert time.time() - t1 < 2.0
