@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-pmc_r04}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-KV="$R/tools/kernel_variants.py --configs 2 --batches 1024 --reps 30 --variants default --precision fp32"
+KV="$R/tools/kernel_variants.py --configs 2 --batches 1024 --reps 30 --variants default --precision bf16x3"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 $KV > $OUT/fetch.log 2>&1 || { echo "fetch pass failed"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 $KV > $OUT/write.log 2>&1 || { echo "write pass failed"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
