@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--configs", default="1,2,3")
     ap.add_argument("--variants", default=",".join(VARIANTS))
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "bf16x3", "split", "fp32"])
     args = ap.parse_args()
     batches = [int(b) for b in args.batches.split(",")]
     for cfg in [int(c) for c in args.configs.split(",")]:
