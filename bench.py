@@ -58,17 +58,19 @@ TRAFFIC_SOURCE = {
                                            "separate passes, 1024-row launches; FETCH x2 gfx950 correction, 1 KB units)",
     "gznn::trunk_kernel_w8<128, 4, 3>": "profiles/r04u_pmc_summary.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                                          "separate passes, 1024-row launches; FETCH x2 gfx950 correction, 1 KB units)",
-    "gznn::trunk_kernel_h2<128, 4, 3>": "profiles/r05b_pmc_summary.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
-                                         "separate passes, 1024-row launches; FETCH x2 gfx950 correction, 1 KB units)"}
+    "gznn::trunk_kernel_h2<128, 4, 3>": "profiles/r06m_pmc_summary.txt (the final tree; rocprofv3 --pmc FETCH_SIZE / "
+                                         "WRITE_SIZE, separate passes, 1024-row launches; FETCH x2 gfx950 correction, "
+                                         "1 KB units; round 5's r05b_pmc_summary.txt: identical)"}
 
 
 PEAK_HBM_GBPS = 8000.0         # MI355X HBM3E (MI355X_MICROARCH.md)
 # SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE (summed over the 8 XCDs) per launch of the dominant
 # kernel at 1,024 rows, from one rocprofv3 --pmc pass (tools/gpu_pmc_r04.sh)
 PMC_PER_LAUNCH = {"gznn::trunk_kernel_h2<128, 4, 3>": {
-    "mfma_busy_cycles": 682622976.0, "grbm_gui_active": 9249473.5,
-    "source": "profiles/r05b_pmc_summary.txt (rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES ... GRBM_GUI_ACTIVE, one pass, "
-              "1024-row launches, tools/gpu_pmc_r04.sh): busy cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)"},
+    "mfma_busy_cycles": 682622976.0, "grbm_gui_active": 9254898.8,
+    "source": "profiles/r06m_pmc_summary.txt (the final tree; rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES ... GRBM_GUI_ACTIVE, "
+              "one pass, 1024-row launches, tools/gpu_pmc_r04.sh; round 5's r05b_pmc_summary.txt: the same kernel, "
+              "9249473.5 active cycles): busy cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)"},
     "gznn::trunk_kernel_w8<128, 4, 3>": {
     "mfma_busy_cycles": 682622976.0, "grbm_gui_active": 8828934.5,
     "source": "profiles/r04u_pmc_summary.txt (rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES ... GRBM_GUI_ACTIVE, one pass, "
